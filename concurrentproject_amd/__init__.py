@@ -1,0 +1,243 @@
+"""concurrentproject_amd -- MI355X (gfx950) Smith-Waterman score engine.
+
+Python mirror of the reference's score interface (algoGPU.h:1-14 and the
+harness calls of TestFileWithGPU.cpp:81-94) over the C-ABI of
+``libswmi355.so`` (include/algoGPU.h).  Every call goes to the HIP kernels; there
+is no CPU fallback: if the library is missing, importing the engine raises.
+
+    import concurrentproject_amd as sw
+    sw.SmithWatermanScoreCUDA(b"GATTACA", b"GCATGCU")      # -> 2
+    sw.score_batch([(a0, b0), (a1, b1)])                     # -> [s0, s1]
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass
+from typing import Iterable, Sequence
+
+import numpy as np
+
+__all__ = [
+    "Params", "lib", "build", "SequentialSmithWatermanScoreGPU", "SmithWatermanLazyGPU",
+    "SmithWatermanScoreCUDA", "SmithDiagonalGPU", "score", "score_batch", "score_batch_device",
+    "set_params", "get_params", "set_option", "get_option", "last_stats", "gen_pair", "gen_batch",
+    "SwError", "LIB_PATH",
+]
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libswmi355.so")
+SW_FLAG_DNA, SW_FLAG_BYTES = 1, 2
+
+
+class SwError(RuntimeError):
+    """A failed engine call (the C-ABI returned -1); the message is sw_last_error()."""
+
+
+@dataclass(frozen=True)
+class Params:
+    """Scoring constants (main.cpp:20-23 defaults)."""
+    match: int = 1
+    mismatch: int = -1
+    gap_init: int = 1
+    gap_ext: int = 1
+
+
+class _Stats(ctypes.Structure):
+    _fields_ = [("kernel_ms", ctypes.c_float), ("total_ms", ctypes.c_float), ("cells", ctypes.c_longlong),
+                ("W", ctypes.c_int), ("C", ctypes.c_int), ("dna", ctypes.c_int), ("blocks", ctypes.c_int),
+                ("waves_per_cu", ctypes.c_int), ("items", ctypes.c_int), ("boundary_bytes", ctypes.c_longlong)]
+
+
+_lib = None
+
+
+def build(verbose: bool = False) -> str:
+    """Compile libswmi355.so in-tree for gfx950 (hipcc; no GPU needed)."""
+    import subprocess
+    cmd = ["make", "-C", os.path.join(HERE, "csrc")]
+    if not verbose:
+        cmd.insert(1, "-s")
+    subprocess.run(cmd, check=True)
+    return LIB_PATH
+
+
+def lib() -> ctypes.CDLL:
+    """The loaded engine.  Raises if libswmi355.so has not been built (no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError("libswmi355.so not built: run concurrentproject_amd.build() "
+                          "(hipcc --offload-arch=gfx950); there is no CPU fallback")
+    L = ctypes.CDLL(LIB_PATH)
+    u8p = ctypes.POINTER(ctypes.c_ubyte)
+    i = ctypes.c_int
+    for name in ("SequentialSmithWatermanScoreGPU", "SmithWatermanLazyGPU", "SmithWatermanScoreCUDA",
+                 "SmithDiagonalGPU"):
+        f = getattr(L, name)
+        f.argtypes = [u8p, u8p, i, i]
+        f.restype = i
+    L.sw_set_params.argtypes = [i, i, i, i]
+    L.sw_set_params.restype = i
+    L.sw_get_params.argtypes = [ctypes.POINTER(i)] * 4
+    L.sw_score_params.argtypes = [u8p, u8p, i, i, i, i, i, i]
+    L.sw_score_params.restype = i
+    L.sw_score_batch.argtypes = [ctypes.POINTER(u8p), ctypes.POINTER(i), ctypes.POINTER(u8p),
+                                 ctypes.POINTER(i), i, ctypes.POINTER(i)]
+    L.sw_score_batch.restype = i
+    L.sw_score_batch_device.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(i),
+                                        ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(i), i, ctypes.c_void_p, i,
+                                        ctypes.c_void_p]
+    L.sw_score_batch_device.restype = i
+    L.sw_stream_status.argtypes = [ctypes.c_void_p]
+    L.sw_stream_status.restype = i
+    L.sw_set_option.argtypes = [ctypes.c_char_p, ctypes.c_longlong]
+    L.sw_set_option.restype = i
+    L.sw_get_option.argtypes = [ctypes.c_char_p]
+    L.sw_get_option.restype = ctypes.c_longlong
+    L.sw_last_stats.argtypes = [ctypes.POINTER(_Stats)]
+    L.sw_last_stats.restype = i
+    L.sw_last_error.restype = ctypes.c_char_p
+    L.sw_version.restype = i
+    L.sw_gen_pair.argtypes = [ctypes.c_uint64, i, u8p, u8p]
+    L.sw_gen_batch.argtypes = [ctypes.c_uint64, i, i, u8p]
+    _lib = L
+    return L
+
+
+def _u8(a) -> np.ndarray:
+    if isinstance(a, str):
+        a = a.encode("latin-1")
+    if isinstance(a, (bytes, bytearray, memoryview)):
+        return np.frombuffer(bytes(a), dtype=np.uint8)
+    return np.ascontiguousarray(a, dtype=np.uint8)
+
+
+def _ptr(arr: np.ndarray):
+    return arr.ctypes.data_as(ctypes.POINTER(ctypes.c_ubyte))
+
+
+def _check(rc: int) -> int:
+    if rc < 0:
+        raise SwError(lib().sw_last_error().decode(errors="replace"))
+    return rc
+
+
+def _pair_call(fname: str, seq1, seq2) -> int:
+    a, b = _u8(seq1), _u8(seq2)
+    return _check(getattr(lib(), fname)(_ptr(a), _ptr(b), len(a), len(b)))
+
+
+# ---- the reference's algoGPU.h surface ----------------------------------------------------
+
+def SequentialSmithWatermanScoreGPU(seq1, seq2) -> int:
+    """algoGPU.h:5 (simpleGPU.cu:109): score of (seq1, seq2)."""
+    return _pair_call("SequentialSmithWatermanScoreGPU", seq1, seq2)
+
+
+def SmithWatermanLazyGPU(seq1, seq2) -> int:
+    """algoGPU.h:7 (cudaLazy.cu:58)."""
+    return _pair_call("SmithWatermanLazyGPU", seq1, seq2)
+
+
+def SmithWatermanScoreCUDA(seq1, seq2) -> int:
+    """algoGPU.h:9 (cudaSmithM.cu:128)."""
+    return _pair_call("SmithWatermanScoreCUDA", seq1, seq2)
+
+
+def SmithDiagonalGPU(seq1, seq2) -> int:
+    """SmithDiagonalGPUrefactored.cu:174 (linear gap = G_INIT per residue)."""
+    return _pair_call("SmithDiagonalGPU", seq1, seq2)
+
+
+# ---- extensions ---------------------------------------------------------------------------
+
+def score(seq1, seq2, params: Params | None = None) -> int:
+    """Best local-alignment score; ``params`` overrides the process-wide constants for this call."""
+    if params is None:
+        return SmithWatermanScoreCUDA(seq1, seq2)
+    a, b = _u8(seq1), _u8(seq2)
+    return _check(lib().sw_score_params(_ptr(a), _ptr(b), len(a), len(b), params.match, params.mismatch,
+                                        params.gap_init, params.gap_ext))
+
+
+def score_batch(pairs: Iterable[Sequence], params: Params | None = None) -> list:
+    """Scores of many independent pairs in one launch."""
+    arrs = [(_u8(a), _u8(b)) for a, b in pairs]
+    n = len(arrs)
+    if n == 0:
+        return []
+    u8p = ctypes.POINTER(ctypes.c_ubyte)
+    A = (u8p * n)(*[_ptr(x) for x, _ in arrs])
+    B = (u8p * n)(*[_ptr(y) for _, y in arrs])
+    AL = (ctypes.c_int * n)(*[len(x) for x, _ in arrs])
+    BL = (ctypes.c_int * n)(*[len(y) for _, y in arrs])
+    out = (ctypes.c_int * n)()
+    old = None
+    if params is not None:
+        old = get_params()
+        set_params(params)
+    try:
+        _check(lib().sw_score_batch(A, AL, B, BL, n, out))
+    finally:
+        if old is not None:
+            set_params(old)
+    return list(out)
+
+
+def score_batch_device(d_arena_ptr: int, a_off, alen, b_off, blen, d_scores_ptr: int, flags: int = 0,
+                       stream: int | None = None) -> None:
+    """Sequences already in device memory (arena pointer + byte offsets).  Asynchronous on ``stream``."""
+    npairs = len(alen)
+    ao = (ctypes.c_int64 * npairs)(*[int(x) for x in a_off])
+    bo = (ctypes.c_int64 * npairs)(*[int(x) for x in b_off])
+    al = (ctypes.c_int * npairs)(*[int(x) for x in alen])
+    bl = (ctypes.c_int * npairs)(*[int(x) for x in blen])
+    _check(lib().sw_score_batch_device(ctypes.c_void_p(d_arena_ptr), ao, al, bo, bl, npairs,
+                                       ctypes.c_void_p(d_scores_ptr), flags,
+                                       ctypes.c_void_p(stream) if stream else None))
+
+
+def stream_status(stream: int | None = None) -> None:
+    _check(lib().sw_stream_status(ctypes.c_void_p(stream) if stream else None))
+
+
+def set_params(p: Params) -> None:
+    _check(lib().sw_set_params(p.match, p.mismatch, p.gap_init, p.gap_ext))
+
+
+def get_params() -> Params:
+    v = [ctypes.c_int() for _ in range(4)]
+    lib().sw_get_params(*[ctypes.byref(x) for x in v])
+    return Params(*[x.value for x in v])
+
+
+def set_option(key: str, value: int) -> None:
+    if lib().sw_set_option(key.encode(), int(value)) != 0:
+        raise SwError("bad option %s=%r" % (key, value))
+
+
+def get_option(key: str) -> int:
+    return int(lib().sw_get_option(key.encode()))
+
+
+def last_stats() -> dict:
+    s = _Stats()
+    lib().sw_last_stats(ctypes.byref(s))
+    return {k: getattr(s, k) for k, _ in _Stats._fields_}
+
+
+def gen_pair(seed: int, length: int) -> tuple:
+    """cudaSmithM.cu:200-212 synthetic pair: mt19937_64(seed), a[i] then b[i] over 'ACGT'."""
+    a = np.empty(length, dtype=np.uint8)
+    b = np.empty(length, dtype=np.uint8)
+    lib().sw_gen_pair(seed, length, _ptr(a), _ptr(b))
+    return a, b
+
+
+def gen_batch(seed_base: int, npairs: int, length: int) -> np.ndarray:
+    """npairs pairs (pair k seeded seed_base+k) as one arena [a_0|b_0|a_1|b_1|...]."""
+    arena = np.empty(2 * length * npairs, dtype=np.uint8)
+    lib().sw_gen_batch(seed_base, npairs, length, _ptr(arena))
+    return arena

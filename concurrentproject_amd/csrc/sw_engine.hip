@@ -1,0 +1,677 @@
+// sw_engine.hip -- C++ host layer of libswmi355.so: the drop-in C-ABI of
+// include/algoGPU.h over the gfx950 strip kernel (sw_kernels.hip).
+//
+// Replaces the host drivers of the reference GPU engines
+// (simpleGPU.cu:109-163, cudaLazy.cu:58-99, cudaSmithM.cu:128-189,
+// SmithDiagonalGPUrefactored.cu:174-230).  Differences that are deliberate:
+//   * one persistent launch per call instead of m+n-1 launches;
+//   * no (m+1)(n+1) matrices: device state is O(n) per pair plus one strip
+//     boundary column per strip (H-G_INIT, E-G_EXT per row);
+//   * the max is reduced on the device; one int per pair comes back;
+//   * every HIP call is checked; failures return -1 with sw_last_error();
+//   * device memory and a non-blocking stream are cached per (thread, device).
+#include "sw_internal.h"
+#include "../../include/algoGPU.h"
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <string>
+#include <vector>
+
+namespace swmi {
+namespace {
+
+thread_local std::string t_err;
+thread_local sw_stats t_stats{};
+
+void set_err(const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    t_err = buf;
+}
+
+#define HIPCHK(expr)                                                                   \
+    do {                                                                               \
+        hipError_t e_ = (expr);                                                        \
+        if (e_ != hipSuccess) {                                                        \
+            set_err("%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__, __LINE__); \
+            return -1;                                                                 \
+        }                                                                              \
+    } while (0)
+
+struct Params {
+    int match = 1, mismatch = -1, gap_init = 1, gap_ext = 1;   // main.cpp:20-23
+};
+
+std::mutex g_param_mu;
+Params g_params;
+
+std::atomic<long long> g_opt_W{0}, g_opt_C{0}, g_opt_bytes{0}, g_opt_timeout{30}, g_opt_blocks{0};
+
+bool params_ok(const Params& p) {
+    if (p.gap_init < 0 || p.gap_ext < 0 || p.gap_init > (1 << 20) || p.gap_ext > (1 << 20)) {
+        set_err("unsupported gap penalties (%d, %d): need 0 <= G_INIT, G_EXT <= 2^20", p.gap_init, p.gap_ext);
+        return false;
+    }
+    if (p.mismatch > 0 || p.mismatch < -127 || p.match > 127 || p.match < p.mismatch) {
+        set_err("unsupported scores (MATCH %d, MISMATCH %d): need -127 <= MISMATCH <= 0, MISMATCH <= MATCH <= 127",
+                p.match, p.mismatch);
+        return false;
+    }
+    return true;
+}
+
+template <class T>
+struct DevBuf {
+    T* p = nullptr;
+    size_t cap = 0;   // elements
+    int ensure(size_t n, hipStream_t sync_first) {
+        if (n <= cap && p) return 0;
+        if (p) {
+            HIPCHK(hipStreamSynchronize(sync_first));
+            HIPCHK(hipFree(p));
+            p = nullptr;
+            cap = 0;
+        }
+        size_t want = std::max<size_t>(n, 1);
+        want = want + want / 4;   // grow with slack
+        HIPCHK(hipMalloc((void**)&p, want * sizeof(T)));
+        cap = want;
+        return 0;
+    }
+};
+
+template <class T>
+struct PinBuf {
+    T* p = nullptr;
+    size_t cap = 0;
+    int ensure(size_t n) {
+        if (n <= cap && p) return 0;
+        if (p) { HIPCHK(hipHostFree(p)); p = nullptr; cap = 0; }
+        size_t want = std::max<size_t>(n, 1);
+        want = want + want / 4;
+        HIPCHK(hipHostMalloc((void**)&p, want * sizeof(T), hipHostMallocDefault));
+        cap = want;
+        return 0;
+    }
+};
+
+struct Ctx {
+    int dev = -1;
+    int cus = 256;
+    hipStream_t own = nullptr;        // engine stream for synchronous calls
+    hipStream_t last = nullptr;       // stream of the previous call
+    hipEvent_t ev0 = nullptr, ev1 = nullptr, staged = nullptr;
+    bool staged_pending = false;
+    DevBuf<unsigned char> seq;
+    DevBuf<PairDesc> desc;
+    DevBuf<int> ibase;
+    DevBuf<Granule> bnd;
+    DevBuf<Ctrl> ctrl;
+    DevBuf<int> scores;
+    DevBuf<unsigned> flag;
+    PinBuf<unsigned char> hseq;
+    PinBuf<PairDesc> hdesc;
+    PinBuf<int> hibase;
+    PinBuf<int> hscores;
+    PinBuf<Ctrl> hctrl;
+    unsigned epoch = 0;
+    std::map<int, int> waves_cache;   // variant key -> waves per CU
+};
+
+thread_local std::map<int, Ctx*> t_ctx;
+
+Ctx* get_ctx() {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) {
+        set_err("hipGetDevice failed: no HIP device");
+        return nullptr;
+    }
+    auto it = t_ctx.find(dev);
+    if (it != t_ctx.end()) return it->second;
+    Ctx* c = new Ctx();
+    c->dev = dev;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, dev) != hipSuccess) {
+        set_err("hipGetDeviceProperties failed");
+        delete c;
+        return nullptr;
+    }
+    c->cus = prop.multiProcessorCount;
+    if (hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
+        hipEventCreateWithFlags(&c->staged, hipEventDisableTiming) != hipSuccess) {
+        set_err("stream/event creation failed");
+        delete c;
+        return nullptr;
+    }
+    t_ctx[dev] = c;
+    return c;
+}
+
+// ---- problem description -------------------------------------------------
+
+struct Job {
+    // per active pair, after orientation
+    std::vector<PairDesc> pairs;
+    std::vector<int> item_base;
+    long long cells = 0;
+    uint64_t bnd_granules = 0;
+    int W = 1, C = 16;
+    bool dna = true;
+};
+
+bool is_dna_byte(unsigned char c) { return c == 'A' || c == 'C' || c == 'G' || c == 'T'; }
+
+bool all_dna(const unsigned char* s, int len) {
+    for (int i = 0; i < len; ++i)
+        if (!is_dna_byte(s[i])) return false;
+    return true;
+}
+
+int pick_W(const std::vector<PairDesc>& pairs, bool single) {
+    long long forced = g_opt_W.load();
+    if (forced) return (int)forced;
+    if (single) {
+        // single pair: enough strips to put ~1-2 waves on every SIMD while
+        // keeping the per-step instruction stream short (the anti-diagonal
+        // critical path is paid per step).  DESIGN.md, "Choosing W".
+        const int n = pairs[0].n;
+        for (int W : {1, 2, 4, 8})
+            if ((n + 64 * W - 1) / (64 * W) <= 2048) return W;
+        return 8;
+    }
+    // batch: inter-pair parallelism fills the GPU; amortise the per-step
+    // overhead (W) against the per-strip fill (64W steps per m rows).
+    std::vector<int> ns;
+    ns.reserve(pairs.size());
+    for (auto& p : pairs) ns.push_back(std::min(p.n, p.m));
+    std::nth_element(ns.begin(), ns.begin() + ns.size() / 2, ns.end());
+    const int med = ns[ns.size() / 2];
+    if (med >= 4096) return 8;
+    if (med >= 1024) return 4;
+    if (med >= 256) return 2;
+    return 1;
+}
+
+int pick_C(int W) {
+    long long forced = g_opt_C.load();
+    if (forced) return (int)forced;
+    return W == 1 ? 16 : W == 2 ? 32 : 64;
+}
+
+// Build descriptors for `np` pairs given their (col, row) lengths and arena
+// offsets.  `single` selects the single-pair orientation policy.
+void plan(Job& job, int W, int C) {
+    job.W = W;
+    job.C = C;
+    job.item_base.assign(job.pairs.size() + 1, 0);
+    uint64_t g = 0;
+    long long cells = 0;
+    for (size_t k = 0; k < job.pairs.size(); ++k) {
+        PairDesc& d = job.pairs[k];
+        d.strips = (d.n + 64 * W - 1) / (64 * W);
+        d.bnd_off = g;
+        g += (uint64_t)(d.strips - 1) * (uint64_t)d.m;
+        job.item_base[k + 1] = job.item_base[k] + d.strips;
+        cells += (long long)d.n * (long long)d.m;
+    }
+    job.bnd_granules = g;
+    job.cells = cells;
+}
+
+void profile_words(const Params& p, unsigned out[4]) {
+    for (int q = 0; q < 4; ++q) {
+        unsigned w = 0;
+        for (int r = 0; r < 4; ++r) {
+            const int s = (r == q ? p.match : p.mismatch) + 128;
+            w |= (unsigned)(s & 0xFF) << (8 * r);
+        }
+        out[q] = w;
+    }
+}
+
+int waves_per_cu(Ctx* c, const LaunchCfg& cfg) {
+    const int key = cfg.W * 1000 + cfg.C * 2 + (cfg.dna ? 1 : 0);
+    auto it = c->waves_cache.find(key);
+    if (it != c->waves_cache.end()) return it->second;
+    int w = kernel_waves_per_cu(cfg);
+    if (w <= 0) w = 4;
+    c->waves_cache[key] = w;
+    return w;
+}
+
+// Enqueue the launch for a planned job whose sequences are in `d_seq`.
+int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int* d_scores, int nscores,
+            hipStream_t s, bool time_kernel) {
+    if (!variant_exists(job.W, job.C)) {
+        set_err("no kernel variant for W=%d C=%d", job.W, job.C);
+        return -1;
+    }
+    const size_t np = job.pairs.size();
+    // staging buffers may still be read by the previous call's async copies
+    if (c->staged_pending) {
+        HIPCHK(hipEventSynchronize(c->staged));
+        c->staged_pending = false;
+    }
+    if (c->hdesc.ensure(np) || c->hibase.ensure(np + 1)) return -1;
+    std::memcpy(c->hdesc.p, job.pairs.data(), np * sizeof(PairDesc));
+    std::memcpy(c->hibase.p, job.item_base.data(), (np + 1) * sizeof(int));
+    if (c->desc.ensure(np, s) || c->ibase.ensure(np + 1, s) || c->ctrl.ensure(1, s)) return -1;
+    if (job.bnd_granules) {
+        size_t freeb = 0, totb = 0;
+        HIPCHK(hipMemGetInfo(&freeb, &totb));
+        const size_t need = job.bnd_granules * sizeof(Granule);
+        if (need > c->bnd.cap * sizeof(Granule) && need > freeb / 10 * 9) {
+            set_err("strip-boundary buffers need %.2f GB, %.2f GB free", need / 1e9, freeb / 1e9);
+            return -1;
+        }
+        if (c->bnd.ensure(job.bnd_granules, s)) return -1;
+    }
+    HIPCHK(hipMemcpyAsync(c->desc.p, c->hdesc.p, np * sizeof(PairDesc), hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(c->ibase.p, c->hibase.p, (np + 1) * sizeof(int), hipMemcpyHostToDevice, s));
+    HIPCHK(hipEventRecord(c->staged, s));
+    c->staged_pending = true;
+    HIPCHK(hipMemsetAsync(c->ctrl.p, 0, sizeof(unsigned), s));   // next_item only; error stays sticky
+    HIPCHK(hipMemsetAsync(d_scores, 0, (size_t)nscores * sizeof(int), s));
+
+    LaunchCfg cfg{job.W, job.C, job.dna, 0};
+    const int wpc = waves_per_cu(c, cfg);
+    const int items = job.item_base[np];
+    long long blocks = g_opt_blocks.load();
+    if (blocks <= 0) {
+        const long long cap = (long long)c->cus * std::max(1, wpc / 4);
+        blocks = std::min<long long>((items + 3) / 4, cap);
+    }
+    cfg.blocks = (int)std::max<long long>(1, blocks);
+
+    KParams kp{};
+    kp.seq = d_seq;
+    kp.pairs = c->desc.p;
+    kp.item_base = c->ibase.p;
+    kp.bnd = c->bnd.p;
+    kp.ctrl = c->ctrl.p;
+    kp.scores = d_scores;
+    kp.npairs = (int)np;
+    kp.total_items = items;
+    if (++c->epoch == 0) ++c->epoch;
+    kp.epoch = c->epoch;
+    kp.match = prm.match;
+    kp.mismatch = prm.mismatch;
+    kp.gap_init = prm.gap_init;
+    kp.gap_ext = prm.gap_ext;
+    profile_words(prm, kp.prof);
+    kp.timeout_ticks = g_opt_timeout.load() * 100000000LL;   // s_memrealtime: 100 MHz
+
+    if (time_kernel) HIPCHK(hipEventRecord(c->ev0, s));
+    HIPCHK(launch_sw_strip(cfg, kp, s));
+    if (time_kernel) HIPCHK(hipEventRecord(c->ev1, s));
+
+    t_stats = sw_stats{};
+    t_stats.cells = job.cells;
+    t_stats.W = job.W;
+    t_stats.C = job.C;
+    t_stats.dna = job.dna ? 1 : 0;
+    t_stats.blocks = cfg.blocks;
+    t_stats.waves_per_cu = wpc;
+    t_stats.items = items;
+    t_stats.boundary_bytes = (long long)(job.bnd_granules * sizeof(Granule));
+    c->last = s;
+    return 0;
+}
+
+int check_ctrl(Ctx* c, hipStream_t s) {
+    if (c->hctrl.ensure(1)) return -1;
+    HIPCHK(hipMemcpyAsync(c->hctrl.p, c->ctrl.p, sizeof(Ctrl), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    if (c->hctrl.p->error) {
+        set_err("strip hand-off timed out (error %u, strip %u): a producer strip never published", c->hctrl.p->error,
+                c->hctrl.p->err_item);
+        HIPCHK(hipMemsetAsync(c->ctrl.p, 0, sizeof(Ctrl), s));
+        HIPCHK(hipStreamSynchronize(s));
+        return -1;
+    }
+    return 0;
+}
+
+struct HostPair {
+    const unsigned char* s1;
+    int n;   // seq1 length (reference: columns)
+    const unsigned char* s2;
+    int m;   // seq2 length (reference: rows)
+};
+
+// Synchronous host-buffer path shared by every host API entry.
+int score_host(const HostPair* in, int npairs, const Params& prm, int* out) {
+    const auto t0 = std::chrono::steady_clock::now();
+    if (npairs < 0 || (npairs > 0 && (!in || !out))) {
+        set_err("invalid arguments");
+        return -1;
+    }
+    if (!params_ok(prm)) return -1;
+    for (int k = 0; k < npairs; ++k) {
+        if (in[k].n < 0 || in[k].m < 0 || (in[k].n > 0 && !in[k].s1) || (in[k].m > 0 && !in[k].s2)) {
+            set_err("pair %d: invalid sequence pointer/length", k);
+            return -1;
+        }
+        if ((long long)std::min(in[k].n, in[k].m) * std::max(prm.match, 1) >= (1LL << 28)) {
+            set_err("pair %d: score range exceeds the int32 engine (min length * MATCH >= 2^28)", k);
+            return -1;
+        }
+        out[k] = 0;   // empty pairs score 0 (main.cpp:74-90 with empty loops)
+    }
+    std::vector<int> act;
+    for (int k = 0; k < npairs; ++k)
+        if (in[k].n > 0 && in[k].m > 0) act.push_back(k);
+    if (act.empty()) return 0;
+
+    Ctx* c = get_ctx();
+    if (!c) return -1;
+    hipStream_t s = c->own;
+    if (c->last && c->last != s) HIPCHK(hipStreamSynchronize(c->last));
+
+    Job job;
+    const bool single = act.size() == 1;
+    bool dna = g_opt_bytes.load() == 0;
+    size_t bytes = 0;
+    for (int k : act) {
+        if (dna && !(all_dna(in[k].s1, in[k].n) && all_dna(in[k].s2, in[k].m))) dna = false;
+        bytes += ((size_t)in[k].n + 15) / 16 * 16 + ((size_t)in[k].m + 15) / 16 * 16;
+    }
+    job.dna = dna;
+    if (c->hseq.ensure(bytes)) return -1;
+    // orientation: a single pair spreads its LONGER sequence over lanes (more
+    // strips = more waves); a batch streams its longer sequence as rows (fewer
+    // strip fills per cell).  The score is symmetric either way.
+    size_t off = 0;
+    job.pairs.resize(act.size());
+    for (size_t i = 0; i < act.size(); ++i) {
+        const HostPair& p = in[act[i]];
+        bool swap = single ? (p.m > p.n) : (p.n > p.m);
+        const unsigned char* colp = swap ? p.s2 : p.s1;
+        const unsigned char* rowp = swap ? p.s1 : p.s2;
+        const int n = swap ? p.m : p.n, m = swap ? p.n : p.m;
+        PairDesc& d = job.pairs[i];
+        d.col_off = off;
+        std::memcpy(c->hseq.p + off, colp, (size_t)n);
+        off += ((size_t)n + 15) / 16 * 16;
+        d.row_off = off;
+        std::memcpy(c->hseq.p + off, rowp, (size_t)m);
+        off += ((size_t)m + 15) / 16 * 16;
+        d.n = n;
+        d.m = m;
+        d.out_idx = (int)i;
+    }
+    const int W = pick_W(job.pairs, single);
+    plan(job, W, pick_C(W));
+    if (c->seq.ensure(bytes, s) || c->scores.ensure(act.size(), s) || c->hscores.ensure(act.size())) return -1;
+    HIPCHK(hipMemcpyAsync(c->seq.p, c->hseq.p, bytes, hipMemcpyHostToDevice, s));
+    if (enqueue(c, job, prm, c->seq.p, c->scores.p, (int)act.size(), s, true)) return -1;
+    HIPCHK(hipMemcpyAsync(c->hscores.p, c->scores.p, act.size() * sizeof(int), hipMemcpyDeviceToHost, s));
+    if (check_ctrl(c, s)) return -1;   // synchronises
+    float ms = 0.f;
+    HIPCHK(hipEventElapsedTime(&ms, c->ev0, c->ev1));
+    for (size_t i = 0; i < act.size(); ++i) out[act[i]] = c->hscores.p[i];
+    t_stats.kernel_ms = ms;
+    t_stats.total_ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return 0;
+}
+
+Params current_params() {
+    std::lock_guard<std::mutex> g(g_param_mu);
+    return g_params;
+}
+
+int score_one(const unsigned char* s1, const unsigned char* s2, int n, int m, const Params& prm) {
+    HostPair hp{s1, n, s2, m};
+    int sc = 0;
+    if (score_host(&hp, 1, prm, &sc)) return -1;
+    return sc;
+}
+
+__global__ void alphabet_kernel(const unsigned char* arena, const PairDesc* pairs, int npairs, unsigned* flag) {
+    const int k = blockIdx.x;
+    if (k >= npairs) return;
+    const PairDesc d = pairs[k];
+    unsigned bad = 0;
+    for (int i = threadIdx.x; i < d.n; i += blockDim.x) {
+        const unsigned char ch = arena[d.col_off + i];
+        bad |= !(ch == 'A' || ch == 'C' || ch == 'G' || ch == 'T');
+    }
+    for (int i = threadIdx.x; i < d.m; i += blockDim.x) {
+        const unsigned char ch = arena[d.row_off + i];
+        bad |= !(ch == 'A' || ch == 'C' || ch == 'G' || ch == 'T');
+    }
+    if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(flag, 1u);
+}
+
+}  // namespace
+}  // namespace swmi
+
+using namespace swmi;
+
+extern "C" {
+
+int SequentialSmithWatermanScoreGPU(unsigned char* seq1, unsigned char* seq2, int len1, int len2) {
+    return score_one(seq1, seq2, len1, len2, current_params());
+}
+
+int SmithWatermanLazyGPU(const unsigned char* seq1, const unsigned char* seq2, int n, int m) {
+    return score_one(seq1, seq2, n, m, current_params());
+}
+
+int SmithWatermanScoreCUDA(const unsigned char* seq1, const unsigned char* seq2, int n, int m) {
+    return score_one(seq1, seq2, n, m, current_params());
+}
+
+int SmithDiagonalGPU(unsigned char* seq1, unsigned char* seq2, int n, int m) {
+    Params p = current_params();
+    p.gap_ext = p.gap_init;   // linear gap (SmithDiagonalGPU.cu:59-66)
+    return score_one(seq1, seq2, n, m, p);
+}
+
+int sw_set_params(int match, int mismatch, int gap_init, int gap_ext) {
+    Params p;
+    p.match = match;
+    p.mismatch = mismatch;
+    p.gap_init = gap_init;
+    p.gap_ext = gap_ext;
+    if (!params_ok(p)) return -1;
+    std::lock_guard<std::mutex> g(g_param_mu);
+    g_params = p;
+    return 0;
+}
+
+void sw_get_params(int* match, int* mismatch, int* gap_init, int* gap_ext) {
+    Params p = current_params();
+    if (match) *match = p.match;
+    if (mismatch) *mismatch = p.mismatch;
+    if (gap_init) *gap_init = p.gap_init;
+    if (gap_ext) *gap_ext = p.gap_ext;
+}
+
+int sw_score_params(const unsigned char* seq1, const unsigned char* seq2, int n, int m, int match, int mismatch,
+                    int gap_init, int gap_ext) {
+    Params p;
+    p.match = match;
+    p.mismatch = mismatch;
+    p.gap_init = gap_init;
+    p.gap_ext = gap_ext;
+    return score_one(seq1, seq2, n, m, p);
+}
+
+int sw_score_batch(const unsigned char* const* a, const int* alen, const unsigned char* const* b, const int* blen,
+                   int npairs, int* scores_out) {
+    if (npairs < 0 || (npairs > 0 && (!a || !alen || !b || !blen || !scores_out))) {
+        set_err("sw_score_batch: invalid arguments");
+        return -1;
+    }
+    std::vector<HostPair> v((size_t)npairs);
+    for (int k = 0; k < npairs; ++k) v[k] = HostPair{a[k], alen[k], b[k], blen[k]};
+    return score_host(v.data(), npairs, current_params(), scores_out);
+}
+
+int sw_score_batch_device(const unsigned char* d_arena, const int64_t* a_off, const int* alen, const int64_t* b_off,
+                          const int* blen, int npairs, int* d_scores, int flags, void* stream) {
+    const auto t0 = std::chrono::steady_clock::now();
+    if (npairs <= 0 || !d_arena || !a_off || !alen || !b_off || !blen || !d_scores) {
+        set_err("sw_score_batch_device: invalid arguments");
+        return -1;
+    }
+    const Params prm = current_params();
+    if (!params_ok(prm)) return -1;
+    Ctx* c = get_ctx();
+    if (!c) return -1;
+    hipStream_t s = stream ? (hipStream_t)stream : c->own;
+    if (c->last && c->last != s) HIPCHK(hipStreamSynchronize(c->last));
+    Job job;
+    std::vector<int> idx;   // non-empty pairs; empty ones keep the memset 0
+    for (int k = 0; k < npairs; ++k) {
+        if (alen[k] < 0 || blen[k] < 0 || a_off[k] < 0 || b_off[k] < 0) {
+            set_err("pair %d: negative length/offset", k);
+            return -1;
+        }
+        if ((long long)std::min(alen[k], blen[k]) * std::max(prm.match, 1) >= (1LL << 28)) {
+            set_err("pair %d: score range exceeds the int32 engine", k);
+            return -1;
+        }
+        if (alen[k] > 0 && blen[k] > 0) idx.push_back(k);
+    }
+    job.pairs.resize(idx.size());
+    const bool single = idx.size() == 1;
+    for (size_t i = 0; i < idx.size(); ++i) {
+        const int k = idx[i];
+        bool swap = single ? (blen[k] > alen[k]) : (alen[k] > blen[k]);
+        PairDesc& d = job.pairs[i];
+        d.col_off = (uint64_t)(swap ? b_off[k] : a_off[k]);
+        d.row_off = (uint64_t)(swap ? a_off[k] : b_off[k]);
+        d.n = swap ? blen[k] : alen[k];
+        d.m = swap ? alen[k] : blen[k];
+        d.out_idx = k;
+    }
+    if (job.pairs.empty()) {
+        HIPCHK(hipMemsetAsync(d_scores, 0, (size_t)npairs * sizeof(int), s));
+        if (!stream) HIPCHK(hipStreamSynchronize(s));
+        return 0;
+    }
+    const int W = pick_W(job.pairs, single);
+    plan(job, W, pick_C(W));
+    if (flags & SW_FLAG_BYTES || g_opt_bytes.load()) {
+        job.dna = false;
+    } else if (flags & SW_FLAG_DNA) {
+        job.dna = true;
+    } else {
+        // scan the alphabet on the device (one block per pair)
+        const size_t np = job.pairs.size();
+        if (c->staged_pending) {
+            HIPCHK(hipEventSynchronize(c->staged));
+            c->staged_pending = false;
+        }
+        if (c->hdesc.ensure(np) || c->desc.ensure(np, s) || c->flag.ensure(1, s) || c->hctrl.ensure(1)) return -1;
+        std::memcpy(c->hdesc.p, job.pairs.data(), np * sizeof(PairDesc));
+        HIPCHK(hipMemcpyAsync(c->desc.p, c->hdesc.p, np * sizeof(PairDesc), hipMemcpyHostToDevice, s));
+        HIPCHK(hipMemsetAsync(c->flag.p, 0, sizeof(unsigned), s));
+        hipLaunchKernelGGL(alphabet_kernel, dim3((unsigned)np), dim3(256), 0, s, d_arena, c->desc.p, (int)np, c->flag.p);
+        HIPCHK(hipGetLastError());
+        unsigned* hflag = reinterpret_cast<unsigned*>(c->hctrl.p);
+        HIPCHK(hipMemcpyAsync(hflag, c->flag.p, sizeof(unsigned), hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        job.dna = *hflag == 0;
+    }
+    if (enqueue(c, job, prm, d_arena, d_scores, npairs, s, !stream)) return -1;
+    if (!stream) {
+        if (check_ctrl(c, s)) return -1;
+        float ms = 0.f;
+        HIPCHK(hipEventElapsedTime(&ms, c->ev0, c->ev1));
+        t_stats.kernel_ms = ms;
+    }
+    t_stats.total_ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return 0;
+}
+
+int sw_stream_status(void* stream) {
+    Ctx* c = get_ctx();
+    if (!c) return -1;
+    hipStream_t s = stream ? (hipStream_t)stream : c->own;
+    if (!c->ctrl.p) return 0;
+    return check_ctrl(c, s);
+}
+
+int sw_set_option(const char* key, long long v) {
+    if (!key) return -1;
+    const std::string k(key);
+    if (k == "W") {
+        if (v != 0 && v != 1 && v != 2 && v != 4 && v != 8) return -1;
+        g_opt_W = v;
+    } else if (k == "C") {
+        if (v != 0 && v != 16 && v != 32 && v != 64) return -1;
+        g_opt_C = v;
+    } else if (k == "bytes") {
+        g_opt_bytes = v ? 1 : 0;
+    } else if (k == "timeout") {
+        if (v < 1 || v > 3600) return -1;
+        g_opt_timeout = v;
+    } else if (k == "blocks") {
+        if (v < 0) return -1;
+        g_opt_blocks = v;
+    } else {
+        set_err("unknown option '%s'", key);
+        return -1;
+    }
+    return 0;
+}
+
+long long sw_get_option(const char* key) {
+    if (!key) return -1;
+    const std::string k(key);
+    if (k == "W") return g_opt_W;
+    if (k == "C") return g_opt_C;
+    if (k == "bytes") return g_opt_bytes;
+    if (k == "timeout") return g_opt_timeout;
+    if (k == "blocks") return g_opt_blocks;
+    return -1;
+}
+
+int sw_last_stats(sw_stats* out) {
+    if (!out) return -1;
+    *out = t_stats;
+    return 0;
+}
+
+const char* sw_last_error(void) { return t_err.c_str(); }
+
+int sw_version(void) { return 1; }
+
+}  // extern "C"
+
+// ---- synthetic inputs (bench / harness; not on the score path) -------------
+// std::mt19937_64(seed) with a[i] then b[i] per position (cudaSmithM.cu:204-212).
+// uniform_int_distribution<int>(0,3) over a 64-bit engine is, in libstdc++ 11
+// (bits/uniform_int_dist.h _S_nd), (draw * 4) >> 64 == draw >> 62; written out
+// here so the bytes do not depend on the host's C++ library.
+#include <random>
+extern "C" {
+void sw_gen_pair(uint64_t seed, int len, unsigned char* a, unsigned char* b) {
+    static const char nts[4] = {'A', 'C', 'G', 'T'};
+    std::mt19937_64 g(seed);
+    for (int i = 0; i < len; ++i) {
+        a[i] = (unsigned char)nts[g() >> 62];
+        b[i] = (unsigned char)nts[g() >> 62];
+    }
+}
+// npairs pairs of length len, pair k from seed seed_base + k, laid out
+// [a_0 | b_0 | a_1 | b_1 | ...] in `arena` (2*len*npairs bytes).
+void sw_gen_batch(uint64_t seed_base, int npairs, int len, unsigned char* arena) {
+    for (int k = 0; k < npairs; ++k)
+        sw_gen_pair(seed_base + (uint64_t)k, len, arena + (size_t)2 * len * k, arena + (size_t)2 * len * k + len);
+}
+}

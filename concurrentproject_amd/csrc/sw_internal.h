@@ -1,0 +1,74 @@
+// sw_internal.h -- structures shared by the gfx950 kernels (sw_kernels.hip) and
+// the C++ host layer (sw_engine.hip).  Not part of the public C-ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace swmi {
+
+// One pair after orientation: the "column" sequence (length n) runs across the
+// lanes of a wave, the "row" sequence (length m) streams through it.  The score
+// is symmetric in (seq1, seq2), so the host picks the orientation.
+struct PairDesc {
+    uint64_t col_off;   // byte offset of the column sequence in the sequence arena
+    uint64_t row_off;   // byte offset of the row sequence
+    uint64_t bnd_off;   // granule offset of this pair's strip-boundary buffers
+    int n;              // columns (> 0)
+    int m;              // rows    (> 0)
+    int strips;         // ceil(n / (64*W))
+    int out_idx;        // slot in the score array
+};
+
+// Per-launch control block (zeroed by hipMemsetAsync before every launch).
+struct Ctrl {
+    unsigned int next_item;   // work-claim counter (items claimed strictly in order)
+    unsigned int error;       // nonzero: a bounded spin gave up (see ERR_*)
+    unsigned int err_item;
+    unsigned int pad;
+};
+
+enum : unsigned { ERR_TIMEOUT = 1u };
+
+// A strip boundary hand-off granule: written ONCE per launch with a single
+// 16-byte write-through (sc1) store by the producer wave, read with sc1 loads
+// by the consumer wave.  `tag` carries the launch epoch, `chk` detects a torn
+// or stale read.  (MI355X_MICROARCH.md, Workgroup dispatch ... R2 granules.)
+struct alignas(16) Granule {
+    unsigned int tag;
+    int hg;      // H - G_INIT of the strip's last column at this row
+    int eh;      // E - G_EXT  of the strip's last column at this row
+    unsigned int chk;
+};
+
+__host__ __device__ inline unsigned granule_chk(unsigned tag, int hg, int eh, int row) {
+    return tag ^ (unsigned)hg * 0x85EBCA6Bu ^ (unsigned)eh * 0xC2B2AE35u ^ (unsigned)row * 0x9E3779B9u ^ 0x5BD1E995u;
+}
+
+struct KParams {
+    const unsigned char* seq;     // sequence arena (raw bytes)
+    const PairDesc* pairs;
+    const int* item_base;         // npairs+1 prefix sums of strips
+    Granule* bnd;                 // strip-boundary granule arena
+    Ctrl* ctrl;
+    int* scores;
+    int npairs;
+    int total_items;
+    unsigned epoch;               // != 0, unique per launch
+    int match, mismatch, gap_init, gap_ext;
+    unsigned prof[4];             // DNA mode: per column code, 4 biased score bytes (row code 0..3)
+    long long timeout_ticks;      // s_memrealtime ticks (100 MHz) before a spin gives up
+};
+
+// Host-side launch (sw_kernels.hip).
+struct LaunchCfg {
+    int W;          // columns per lane
+    int C;          // rows per hand-off chunk
+    bool dna;       // 2-bit ACGT profile path (else raw-byte compare)
+    int blocks;     // persistent workgroups (256 threads = 4 independent waves)
+};
+
+hipError_t launch_sw_strip(const LaunchCfg& cfg, const KParams& kp, hipStream_t stream);
+int kernel_waves_per_cu(const LaunchCfg& cfg);     // residency of the chosen variant
+bool variant_exists(int W, int C);
+
+}  // namespace swmi

@@ -1,0 +1,119 @@
+/*
+ * algoGPU.h -- drop-in C-ABI of the MI355X (gfx950) Smith-Waterman score engine
+ * (libswmi355.so).  Link this library in place of the reference's
+ * simpleGPU.o / cudaLazy.o / cudaSmithM.o (reference Makefile2:15) and keep the
+ * reference's TestFileWithGPU.cpp and CPU sources unchanged.
+ *
+ * Semantics shared by every entry point:
+ *   - the return value is the best local-alignment score max H >= 0 of the
+ *     affine-gap recurrence of main.cpp:54-66 (E from the left, F from above,
+ *     borders 0, score byte equality main.cpp:28-33), bit-exact;
+ *   - seq1 has length n (len1), seq2 has length m (len2); the score is
+ *     symmetric; any byte values are allowed (an {A,C,G,T}-only input takes
+ *     the 2-bit profile path, anything else the raw-byte path);
+ *   - n == 0 or m == 0 returns 0 (main.cpp:74-90 with empty loops);
+ *   - the call is synchronous and re-entrant per host thread; the caller owns
+ *     the host buffers, which are only read; device memory and the HIP stream
+ *     are cached per (thread, device) and are not observable;
+ *   - on an internal HIP failure, an invalid argument or unsupported scoring
+ *     constants the return value is -1 and sw_last_error() says why (the
+ *     reference had no error channel; cudaSmithM.cu:168-173 returned a
+ *     partial score instead).
+ *   - the scoring constants default to the reference's
+ *     MATCH=1, MISMATCH=-1, G_INIT=1, G_EXT=1 (main.cpp:20-23) and can be
+ *     changed with sw_set_params().
+ */
+#ifndef SWMI355_ALGOGPU_H
+#define SWMI355_ALGOGPU_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- the reference's algoGPU.h:5-9 surface (exact signatures) ---------------- */
+
+/* replaces simpleGPU.cu:109-163 (reference: one launch + device sync per
+ * anti-diagonal, only correct for len2 <= len1 and N < 46341). */
+int SequentialSmithWatermanScoreGPU(unsigned char* seq1, unsigned char* seq2, int len1, int len2);
+
+/* replaces cudaLazy.cu:58-99 (reference: full-matrix anti-diagonal kernel). */
+int SmithWatermanLazyGPU(const unsigned char* seq1, const unsigned char* seq2, int n, int m);
+
+/* replaces cudaSmithM.cu:128-189 (reference: full-matrix, no per-diagonal sync). */
+int SmithWatermanScoreCUDA(const unsigned char* seq1, const unsigned char* seq2, int n, int m);
+
+/* replaces SmithDiagonalGPUrefactored.cu:174-230 (extern "C" but never declared
+ * in the reference's algoGPU.h).  That kernel is LINEAR-gap (gap = G_INIT per
+ * residue, SmithDiagonalGPU.cu:59-66); this entry keeps its semantics: it is
+ * the affine engine with G_EXT := G_INIT, which is exactly the linear model. */
+int SmithDiagonalGPU(unsigned char* seq1, unsigned char* seq2, int n, int m);
+
+/* ---- extensions (no reference counterpart) ---------------------------------- */
+
+/* Scoring constants for later calls from ANY thread (process-wide).
+ * Supported: 0 <= gap_init, gap_ext <= 1<<20; -127 <= mismatch <= 0;
+ * mismatch <= match <= 127.  Returns 0, or -1 if unsupported. */
+int sw_set_params(int match, int mismatch, int gap_init, int gap_ext);
+void sw_get_params(int* match, int* mismatch, int* gap_init, int* gap_ext);
+
+/* One pair with explicit constants (does not change the process-wide ones). */
+int sw_score_params(const unsigned char* seq1, const unsigned char* seq2, int n, int m,
+                    int match, int mismatch, int gap_init, int gap_ext);
+
+/* Batch of independent pairs (host buffers); scores_out[k] = score(a[k], b[k]).
+ * One launch for the whole batch.  Returns 0 or -1. */
+int sw_score_batch(const unsigned char* const* a, const int* alen,
+                   const unsigned char* const* b, const int* blen,
+                   int npairs, int* scores_out);
+
+/* Batch whose sequences are already resident in device memory (one arena,
+ * byte offsets per sequence).  Offsets/lengths are HOST arrays; d_scores is a
+ * device array of npairs ints.  Asynchronous on `stream` (a hipStream_t; NULL =
+ * the engine's own stream, and then the call is synchronous).
+ * flags: SW_FLAG_DNA asserts every byte is in {A,C,G,T} (skips the alphabet
+ * scan), SW_FLAG_BYTES forces the raw-byte path.  After an asynchronous call,
+ * sw_stream_status(stream) synchronises and reports kernel-side failures. */
+#define SW_FLAG_DNA   1
+#define SW_FLAG_BYTES 2
+int sw_score_batch_device(const unsigned char* d_arena,
+                          const int64_t* a_off, const int* alen,
+                          const int64_t* b_off, const int* blen,
+                          int npairs, int* d_scores, int flags, void* stream);
+int sw_stream_status(void* stream);
+
+/* Tuning knobs (process-wide).  Keys:
+ *   "W"        columns per lane: 0 = auto, 1, 2, 4, 8
+ *   "C"        rows per strip hand-off chunk: 0 = auto, 16, 32, 64
+ *   "bytes"    1 = force the raw-byte path
+ *   "timeout"  seconds before a stalled strip hand-off gives up (default 30)
+ *   "blocks"   0 = auto persistent grid, else workgroups per launch
+ * Returns 0, or -1 for an unknown key / bad value. */
+int sw_set_option(const char* key, long long value);
+long long sw_get_option(const char* key);
+
+/* Details of the last launch made by this thread (for the harness / bench). */
+typedef struct {
+    float kernel_ms;        /* HIP-event time of the score kernel alone */
+    float total_ms;         /* wall time of the whole call incl. copies */
+    long long cells;        /* sum of n*m over the launched pairs */
+    int W, C, dna, blocks, waves_per_cu, items;
+    long long boundary_bytes;
+} sw_stats;
+int sw_last_stats(sw_stats* out);
+
+const char* sw_last_error(void);
+int sw_version(void);
+
+/* Synthetic {A,C,G,T} inputs (not on the score path): std::mt19937_64(seed),
+ * a[i] then b[i] per position -- the generator of cudaSmithM.cu:200-212. */
+void sw_gen_pair(uint64_t seed, int len, unsigned char* a, unsigned char* b);
+/* npairs pairs, pair k seeded seed_base+k, laid out [a_0|b_0|a_1|b_1|...]. */
+void sw_gen_batch(uint64_t seed_base, int npairs, int len, unsigned char* arena);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SWMI355_ALGOGPU_H */

@@ -1,0 +1,89 @@
+"""CPU: the C-ABI library builds, loads and exports every symbol include/algoGPU.h
+declares.  Only host-side entry points are called (no GPU here)."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _declared_functions():
+    src = open(os.path.join(ROOT, "include", "algoGPU.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    names = re.findall(r"^\s*(?:const\s+)?[A-Za-z_][A-Za-z0-9_ ]*?[\s\*]+([A-Za-z_][A-Za-z0-9_]*)\s*\(", src, flags=re.M)
+    return sorted(set(n for n in names if n not in ("if", "while")))
+
+
+def test_header_declares_reference_surface():
+    names = _declared_functions()
+    for ref in ("SequentialSmithWatermanScoreGPU", "SmithWatermanLazyGPU", "SmithWatermanScoreCUDA"):
+        assert ref in names
+
+
+def test_library_exports_every_declared_symbol():
+    import concurrentproject_amd as sw
+    if not os.path.exists(sw.LIB_PATH):
+        sw.build()
+    L = ctypes.CDLL(sw.LIB_PATH)
+    missing = [n for n in _declared_functions() if not hasattr(L, n)]
+    assert not missing, missing
+
+
+def test_reference_signatures_exact():
+    """algoGPU.h:5-9 of the reference: argument types and order."""
+    src = open(os.path.join(ROOT, "include", "algoGPU.h")).read()
+    assert "int SequentialSmithWatermanScoreGPU(unsigned char* seq1, unsigned char* seq2, int len1, int len2);" in src
+    assert "int SmithWatermanLazyGPU(const unsigned char* seq1, const unsigned char* seq2, int n, int m);" in src
+    assert "int SmithWatermanScoreCUDA(const unsigned char* seq1, const unsigned char* seq2, int n, int m);" in src
+
+
+def test_param_validation_host_side():
+    import concurrentproject_amd as sw
+    L = sw.lib()
+    assert L.sw_set_params(1, -1, 1, 1) == 0
+    assert L.sw_set_params(2, -3, 5, 2) == 0
+    assert sw.get_params() == sw.Params(2, -3, 5, 2)
+    assert L.sw_set_params(1, 1, 1, 1) == -1        # positive mismatch unsupported
+    assert b"MISMATCH" in L.sw_last_error()
+    assert L.sw_set_params(1, -1, -1, 1) == -1       # negative gap penalty
+    assert sw.get_params() == sw.Params(2, -3, 5, 2)  # unchanged on failure
+    assert L.sw_set_params(1, -1, 1, 1) == 0
+
+
+def test_options_host_side():
+    import concurrentproject_amd as sw
+    for k, v in (("W", 2), ("C", 32), ("timeout", 10), ("blocks", 0), ("bytes", 0)):
+        sw.set_option(k, v)
+        assert sw.get_option(k) == v
+    with pytest.raises(sw.SwError):
+        sw.set_option("W", 3)
+    with pytest.raises(sw.SwError):
+        sw.set_option("nope", 1)
+    sw.set_option("W", 0); sw.set_option("C", 0); sw.set_option("timeout", 30)
+
+
+def test_product_generator_matches_oracle(oracle_mod, golden):
+    """The library's synthetic generator (bench inputs) == the pinned oracle generator."""
+    import concurrentproject_amd as sw
+    for seed, n in ((1024, 1024), (8192, 777), (12345, 5)):
+        a, b = sw.gen_pair(seed, n)
+        oa, ob = oracle_mod.gen_pair(seed, n)
+        assert np.array_equal(a, oa) and np.array_equal(b, ob)
+    arena = sw.gen_batch(8192, 3, 100)
+    for k in range(3):
+        oa, ob = oracle_mod.gen_pair(8192 + k, 100)
+        assert np.array_equal(arena[200 * k:200 * k + 100], oa)
+        assert np.array_equal(arena[200 * k + 100:200 * k + 200], ob)
+
+
+def test_no_oracle_in_product():
+    """The product package never imports the oracle."""
+    pkg = os.path.join(ROOT, "concurrentproject_amd")
+    for dp, _, fs in os.walk(pkg):
+        for f in fs:
+            if f.endswith((".py", ".hip", ".cpp", ".h")):
+                txt = open(os.path.join(dp, f)).read()
+                assert "import oracle" not in txt and "sworacle" not in txt, f

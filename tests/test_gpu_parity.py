@@ -1,0 +1,190 @@
+"""GPU parity: the HIP engine (through the C-ABI) against the oracle and the
+committed golden fixtures.  Bit-exact integer equality everywhere."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ACGT = np.frombuffer(b"ACGT", np.uint8)
+
+
+def _rand_dna(rng, n):
+    return ACGT[rng.integers(0, 4, n)]
+
+
+@pytest.fixture(autouse=True)
+def _defaults(engine):
+    engine.set_params(engine.Params())
+    for k in ("W", "C", "bytes", "blocks"):
+        engine.set_option(k, 0)
+    yield
+    engine.set_params(engine.Params())
+    for k in ("W", "C", "bytes", "blocks"):
+        engine.set_option(k, 0)
+
+
+def test_kats_every_entry_point(engine, golden):
+    g = golden("kat.json")
+    fns = (engine.SequentialSmithWatermanScoreGPU, engine.SmithWatermanLazyGPU,
+           engine.SmithWatermanScoreCUDA, engine.SmithDiagonalGPU)
+    for c in g["cases"]:
+        for f in fns:
+            assert f(c["seq1"], c["seq2"]) == c["score"], (f.__name__, c["seq1"][:16], c["seq2"][:16])
+    got = engine.score_batch([(c["seq1"], c["seq2"]) for c in g["cases"]])
+    assert got == [c["score"] for c in g["cases"]]
+
+
+def test_raw_byte_cases(engine, golden):
+    g = golden("kat.json")["byte_cases"]
+    pairs = [(bytes.fromhex(c["seq1_hex"]), bytes.fromhex(c["seq2_hex"])) for c in g]
+    for (a, b), c in zip(pairs, g):
+        assert engine.score(a, b) == c["score"]
+    assert engine.score_batch(pairs) == [c["score"] for c in g]
+
+
+def _regen(oracle_mod, s):
+    st = oracle_mod.Stream(s["stream_seed"])
+    out = []
+    for N in s["lengths"]:
+        if s["order"] == "interleaved":
+            out.append(st.pair(N))
+        else:
+            out.append((st.seq(N), st.seq(N)))
+    return out
+
+
+def test_published_seeded_sets(engine, oracle_mod, golden):
+    """cudaSmithM.cu:278-363 (published), cudaCompareSmith.cu:122-141, CPUtesting.cpp:131-142."""
+    for s in golden("seeded.json")["sets"]:
+        pairs = _regen(oracle_mod, s)
+        assert [engine.SmithWatermanScoreCUDA(a, b) for a, b in pairs] == s["scores"], s["name"]
+        assert engine.score_batch(pairs) == s["scores"], s["name"]
+
+
+def test_testlazygpu_set(engine, oracle_mod, golden):
+    """testLazyGPU_CPU.cu:231-243: 20 pairs, N = 5000..24000."""
+    s = golden("seeded_lazygpu.json")["sets"][0]
+    pairs = _regen(oracle_mod, s)
+    assert [engine.SmithWatermanLazyGPU(a, b) for a, b in pairs] == s["scores"]
+    assert engine.score_batch(pairs) == s["scores"]
+
+
+def test_params_sets(engine, golden):
+    """G_INIT != G_EXT and other constants (checked in the build container against
+    param-substituted builds of the reference's main.cpp / lazySmith.cpp)."""
+    for s in golden("params.json")["sets"]:
+        p = engine.Params(*s["params"])
+        pairs = [(c["seq1"], c["seq2"]) for c in s["cases"]]
+        exp = [c["score"] for c in s["cases"]]
+        assert [engine.score(a, b, p) for a, b in pairs] == exp, p
+        assert engine.score_batch(pairs, p) == exp, p
+
+
+def test_config_c1(engine, golden):
+    c = golden("configs.json")["C1"]
+    a, b = engine.gen_pair(c["seed"], c["N"])
+    assert engine.SmithWatermanScoreCUDA(a, b) == c["score"] == 124
+
+
+def test_config_c2_single_pair_65536(engine, golden):
+    c = golden("configs.json")["C2"]
+    a, b = engine.gen_pair(c["seed"], c["N"])
+    assert engine.SmithWatermanScoreCUDA(a, b) == c["score"] == 7458
+    # symmetric: the transposed problem gives the same score
+    assert engine.SmithWatermanScoreCUDA(b, a) == c["score"]
+
+
+def test_config_c3_batch_1024(engine, golden):
+    c = golden("configs.json")["C3"]
+    arena = engine.gen_batch(c["seed_base"], c["npairs"], c["N"])
+    N = c["N"]
+    pairs = [(arena[2 * N * k:2 * N * k + N], arena[2 * N * k + N:2 * N * (k + 1)]) for k in range(c["npairs"])]
+    assert engine.score_batch(pairs) == c["scores"]
+
+
+def test_every_variant_ragged(engine, oracle_mod):
+    """Each (W, C) kernel variant, DNA and raw-byte paths, on ragged shapes around
+    the strip widths 64*W and chunk sizes, in one batch and one at a time."""
+    rng = np.random.default_rng(2024)
+    shapes = [(1, 1), (1, 300), (300, 1), (63, 64), (64, 63), (65, 129), (127, 128), (128, 127),
+              (129, 255), (255, 257), (511, 513), (1024, 1000), (2049, 300), (300, 2049), (700, 3000)]
+    pairs = []
+    for n, m in shapes:
+        a = _rand_dna(rng, n)
+        b = _rand_dna(rng, m)
+        if rng.random() < 0.5 and m > 10:   # similar pairs: long alignments cross strips
+            b = np.resize(a, m).copy()
+            mut = rng.random(m) < 0.08
+            b[mut] = _rand_dna(rng, int(mut.sum()))
+        pairs.append((a, b))
+    for prm in (engine.Params(), engine.Params(2, -3, 5, 2), engine.Params(1, -1, 3, 1)):
+        op = oracle_mod.Params(prm.match, prm.mismatch, prm.gap_init, prm.gap_ext)
+        exp = [oracle_mod.score_linear(a, b, op) for a, b in pairs]
+        for W, C in ((1, 16), (1, 32), (2, 32), (4, 64), (8, 64)):
+            engine.set_option("W", W)
+            engine.set_option("C", C)
+            for force_bytes in (0, 1):
+                engine.set_option("bytes", force_bytes)
+                assert engine.score_batch(pairs, prm) == exp, (W, C, force_bytes, prm)
+                for (a, b), e in list(zip(pairs, exp))[::4]:
+                    assert engine.score(a, b, prm) == e, (W, C, force_bytes, len(a), len(b))
+
+
+def test_edges(engine, oracle_mod):
+    assert engine.SmithWatermanScoreCUDA(b"", b"ACGT") == 0
+    assert engine.SmithWatermanScoreCUDA(b"ACGT", b"") == 0
+    assert engine.score_batch([(b"", b""), (b"A", b"A"), (b"", b"A")]) == [0, 1, 0]
+    a = b"A" * 5000
+    assert engine.SmithWatermanScoreCUDA(a, a) == 5000
+    assert engine.SmithWatermanScoreCUDA(b"A" * 3135, b"T" * 3135) == 0
+    # non-ACGT bytes: case-sensitive raw byte equality (main.cpp:28-33)
+    assert engine.score(b"acgt", b"ACGT") == 0
+    assert engine.score(bytes([0, 255, 0, 255]), bytes([0, 255, 0, 255])) == 4
+    # identical long sequences: score = length (long diagonal through every strip)
+    rng = np.random.default_rng(3)
+    s = _rand_dna(rng, 20000)
+    assert engine.score(s, s) == 20000
+    # rectangular single pairs, both orientations
+    x, y = _rand_dna(rng, 9000), _rand_dna(rng, 700)
+    e = oracle_mod.score_linear(x, y)
+    assert engine.score(x, y) == engine.score(y, x) == e
+
+
+def test_linear_entry_point_semantics(engine, oracle_mod):
+    """SmithDiagonalGPU is linear-gap (G_EXT := G_INIT), SmithDiagonalGPU.cu:59-66."""
+    rng = np.random.default_rng(9)
+    engine.set_params(engine.Params(2, -3, 5, 2))
+    for _ in range(5):
+        a, b = _rand_dna(rng, int(rng.integers(50, 900))), _rand_dna(rng, int(rng.integers(50, 900)))
+        assert engine.SmithDiagonalGPU(a, b) == oracle_mod.score_linear(a, b, oracle_mod.Params(2, -3, 5, 5))
+        assert engine.SmithWatermanScoreCUDA(a, b) == oracle_mod.score_linear(a, b, oracle_mod.Params(2, -3, 5, 2))
+
+
+def test_device_resident_batch(engine, oracle_mod):
+    import torch
+    rng = np.random.default_rng(17)
+    seqs, offs, pairs = [], [], []
+    off = 0
+    for _ in range(40):
+        a, b = _rand_dna(rng, int(rng.integers(1, 1500))), _rand_dna(rng, int(rng.integers(1, 1500)))
+        pairs.append((a, b))
+        for s in (a, b):
+            offs.append(off); seqs.append(s); off += len(s)
+    arena = torch.from_numpy(np.concatenate(seqs)).cuda()
+    scores = torch.full((40,), -7, dtype=torch.int32, device="cuda")
+    stream = torch.cuda.current_stream().cuda_stream
+    alen = [len(a) for a, _ in pairs]; blen = [len(b) for _, b in pairs]
+    for flags in (0, 1, 2):
+        engine.score_batch_device(arena.data_ptr(), offs[0::2], alen, offs[1::2], blen, scores.data_ptr(),
+                                  flags=flags, stream=stream)
+        engine.stream_status(stream)
+        exp = [oracle_mod.score_linear(a, b) for a, b in pairs]
+        assert scores.cpu().tolist() == exp, flags
+
+
+def test_errors_are_reported(engine):
+    with pytest.raises(engine.SwError):
+        engine.score(b"ACGT", b"ACGT", engine.Params(1, 2, 1, 1))     # positive mismatch
+    with pytest.raises(engine.SwError):
+        engine.score(b"ACGT", b"ACGT", engine.Params(1, -1, -2, 1))   # negative gap
+    assert engine.score(b"ACGT", b"ACGT") == 4                       # engine still healthy

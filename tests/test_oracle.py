@@ -1,0 +1,86 @@
+"""CPU: the oracle against the reference's own golden vectors and (in the build
+container) against the reference's own main.cpp / lazySmith.cpp."""
+import hashlib
+
+import numpy as np
+import pytest
+
+
+def _sha(a, b):
+    h = hashlib.sha256()
+    h.update(np.asarray(a, np.uint8).tobytes()); h.update(b"|"); h.update(np.asarray(b, np.uint8).tobytes())
+    return h.hexdigest()
+
+
+def test_kats(oracle_mod, golden):
+    g = golden("kat.json")
+    for c in g["cases"]:
+        a, b = c["seq1"], c["seq2"]
+        assert oracle_mod.score_linear(a, b) == c["score"], (a[:20], b[:20])
+        if len(a) * len(b) <= 4000 * 4000:
+            assert oracle_mod.score_full(a, b) == c["score"]
+    for c in g["byte_cases"]:
+        a, b = bytes.fromhex(c["seq1_hex"]), bytes.fromhex(c["seq2_hex"])
+        assert oracle_mod.score_full(a, b) == c["score"]
+
+
+def test_published_seeded_sets(oracle_mod, golden):
+    """cudaSmithM.cu:278-363 published scores, cudaCompareSmith.cu, CPUtesting.cpp."""
+    for s in golden("seeded.json")["sets"]:
+        st = oracle_mod.Stream(s["stream_seed"])
+        for N, exp, h in zip(s["lengths"], s["scores"], s["sha256"]):
+            if s["order"] == "interleaved":
+                a, b = st.pair(N)
+            else:
+                a, b = st.seq(N), st.seq(N)
+            assert _sha(a, b) == h
+            if N <= 4096:
+                assert oracle_mod.score_linear(a, b) == exp
+
+
+def test_params_sets(oracle_mod, golden):
+    for s in golden("params.json")["sets"]:
+        p = oracle_mod.Params(*s["params"])
+        for c in s["cases"][:8]:
+            assert oracle_mod.score_full(c["seq1"], c["seq2"], p) == c["score"]
+            assert oracle_mod.score_linear(c["seq1"], c["seq2"], p) == c["score"]
+
+
+def test_config_c1(oracle_mod, golden):
+    c = golden("configs.json")["C1"]
+    a, b = oracle_mod.gen_pair(c["seed"], c["N"])
+    assert _sha(a, b) == c["sha256"]
+    assert oracle_mod.score_full(a, b) == c["score"] == 124
+
+
+def test_wavefront_equals_linear(oracle_mod):
+    rng = np.random.default_rng(5)
+    for p in (oracle_mod.Params(), oracle_mod.Params(2, -3, 5, 2)):
+        for _ in range(6):
+            n, m = int(rng.integers(1, 700)), int(rng.integers(1, 700))
+            a = np.frombuffer(b"ACGT", np.uint8)[rng.integers(0, 4, n)]
+            b = np.frombuffer(b"ACGT", np.uint8)[rng.integers(0, 4, m)]
+            assert oracle_mod.score_wavefront(a, b, p, threads=4) == oracle_mod.score_linear(a, b, p)
+
+
+def test_restatement_vs_reference_build(oracle_mod):
+    """Only where oracle/_ref exists (build container): the reference's own code."""
+    if oracle_mod.ref_lib() is None:
+        pytest.skip("oracle/_ref not built (no /root/reference here)")
+    rng = np.random.default_rng(11)
+    for _ in range(60):
+        n, m = int(rng.integers(1, 200)), int(rng.integers(1, 200))
+        a = rng.integers(0, 256, n).astype(np.uint8)
+        b = rng.integers(0, 256, m).astype(np.uint8)
+        if rng.random() < 0.7:
+            a = np.frombuffer(b"ACGT", np.uint8)[a % 4]; b = np.frombuffer(b"ACGT", np.uint8)[b % 4]
+        r = oracle_mod.ref_score(a, b)
+        assert oracle_mod.score_full(a, b) == r == oracle_mod.ref_score(a, b, which="lazy")
+    for prm in (oracle_mod.Params(2, -3, 5, 2), oracle_mod.Params(1, -1, 3, 1)):
+        if oracle_mod.ref_lib(prm) is None:
+            continue
+        for _ in range(30):
+            n, m = int(rng.integers(1, 150)), int(rng.integers(1, 150))
+            a = np.frombuffer(b"ACGT", np.uint8)[rng.integers(0, 4, n)]
+            b = np.frombuffer(b"ACGT", np.uint8)[rng.integers(0, 4, m)]
+            assert oracle_mod.score_linear(a, b, prm) == oracle_mod.ref_score(a, b, prm)
