@@ -55,7 +55,16 @@ struct Params {
 std::mutex g_param_mu;
 Params g_params;
 
-std::atomic<long long> g_opt_W{0}, g_opt_C{0}, g_opt_bytes{0}, g_opt_timeout{30}, g_opt_blocks{0};
+std::atomic<long long> g_opt_W{0}, g_opt_C{0}, g_opt_bytes{0}, g_opt_timeout{30}, g_opt_blocks{0}, g_opt_orient{0},
+    g_opt_mode{-1};
+
+// orientation: 0 = engine policy, 1 = seq1 across lanes (columns), 2 = seq2 across lanes
+bool want_swap(bool single, long long len1, long long len2) {
+    const long long o = g_opt_orient.load();
+    if (o == 1) return false;
+    if (o == 2) return true;
+    return single ? (len2 > len1) : (len1 > len2);
+}
 
 bool params_ok(const Params& p) {
     if (p.gap_init < 0 || p.gap_ext < 0 || p.gap_init > (1 << 20) || p.gap_ext > (1 << 20)) {
@@ -167,6 +176,7 @@ struct Job {
     long long cells = 0;
     uint64_t bnd_granules = 0;
     int W = 1, C = 16;
+    int mode = MODE_STRIP;
     bool dna = true;
 };
 
@@ -206,23 +216,36 @@ int pick_W(const std::vector<PairDesc>& pairs, bool single) {
 int pick_C(int W) {
     long long forced = g_opt_C.load();
     if (forced) return (int)forced;
-    return W == 1 ? 16 : W == 2 ? 32 : 64;
+    return W <= 2 ? 32 : 64;   // measured: C=32 beats 16 at W=1 (per-chunk overhead vs lag)
 }
 
 // Build descriptors for `np` pairs given their (col, row) lengths and arena
 // offsets.  `single` selects the single-pair orientation policy.
-void plan(Job& job, int W, int C) {
+int pick_mode(const std::vector<PairDesc>& pairs, bool single) {
+    const long long forced = g_opt_mode.load();
+    if (forced >= 0) return (int)forced;
+    if (single) return pairs[0].strips >= 2 ? MODE_CHAIN : MODE_STRIP;
+    std::vector<int> st;
+    st.reserve(pairs.size());
+    for (auto& p : pairs) st.push_back(p.strips);
+    std::nth_element(st.begin(), st.begin() + st.size() / 2, st.end());
+    return st[st.size() / 2] >= 4 ? MODE_PAIRWG : MODE_STRIP;
+}
+
+void plan(Job& job, int W, int C, bool single) {
     job.W = W;
     job.C = C;
+    for (auto& d : job.pairs) d.strips = (d.n + 64 * W - 1) / (64 * W);
+    job.mode = pick_mode(job.pairs, single);
     job.item_base.assign(job.pairs.size() + 1, 0);
     uint64_t g = 0;
     long long cells = 0;
     for (size_t k = 0; k < job.pairs.size(); ++k) {
         PairDesc& d = job.pairs[k];
-        d.strips = (d.n + 64 * W - 1) / (64 * W);
         d.bnd_off = g;
         g += (uint64_t)(d.strips - 1) * (uint64_t)d.m;
-        job.item_base[k + 1] = job.item_base[k] + d.strips;
+        const int items = job.mode == MODE_CHAIN ? (d.strips + 3) / 4 : job.mode == MODE_PAIRWG ? 1 : d.strips;
+        job.item_base[k + 1] = job.item_base[k] + items;
         cells += (long long)d.n * (long long)d.m;
     }
     job.bnd_granules = g;
@@ -241,7 +264,7 @@ void profile_words(const Params& p, unsigned out[4]) {
 }
 
 int waves_per_cu(Ctx* c, const LaunchCfg& cfg) {
-    const int key = cfg.W * 1000 + cfg.C * 2 + (cfg.dna ? 1 : 0);
+    const int key = cfg.mode * 100000 + cfg.W * 1000 + cfg.C * 2 + (cfg.dna ? 1 : 0);
     auto it = c->waves_cache.find(key);
     if (it != c->waves_cache.end()) return it->second;
     int w = kernel_waves_per_cu(cfg);
@@ -284,13 +307,16 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
     HIPCHK(hipMemsetAsync(c->ctrl.p, 0, sizeof(unsigned), s));   // next_item only; error stays sticky
     HIPCHK(hipMemsetAsync(d_scores, 0, (size_t)nscores * sizeof(int), s));
 
-    LaunchCfg cfg{job.W, job.C, job.dna, 0};
+    LaunchCfg cfg{job.W, job.C, job.dna, 0, job.mode};
     const int wpc = waves_per_cu(c, cfg);
     const int items = job.item_base[np];
     long long blocks = g_opt_blocks.load();
     if (blocks <= 0) {
         const long long cap = (long long)c->cus * std::max(1, wpc / 4);
-        blocks = std::min<long long>((items + 3) / 4, cap);
+        // strip mode: 4 independent waves per block; chain: one block per group;
+        // pair-per-workgroup: one block per pair (grid-stride over pairs)
+        const long long want = job.mode == MODE_STRIP ? (items + 3) / 4 : job.mode == MODE_CHAIN ? items : (long long)np;
+        blocks = std::min<long long>(want, cap);
     }
     cfg.blocks = (int)std::max<long long>(1, blocks);
 
@@ -324,6 +350,7 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
     t_stats.blocks = cfg.blocks;
     t_stats.waves_per_cu = wpc;
     t_stats.items = items;
+    t_stats.mode = job.mode;
     t_stats.boundary_bytes = (long long)(job.bnd_granules * sizeof(Granule));
     c->last = s;
     return 0;
@@ -396,7 +423,7 @@ int score_host(const HostPair* in, int npairs, const Params& prm, int* out) {
     job.pairs.resize(act.size());
     for (size_t i = 0; i < act.size(); ++i) {
         const HostPair& p = in[act[i]];
-        bool swap = single ? (p.m > p.n) : (p.n > p.m);
+        const bool swap = want_swap(single, p.n, p.m);
         const unsigned char* colp = swap ? p.s2 : p.s1;
         const unsigned char* rowp = swap ? p.s1 : p.s2;
         const int n = swap ? p.m : p.n, m = swap ? p.n : p.m;
@@ -412,7 +439,7 @@ int score_host(const HostPair* in, int npairs, const Params& prm, int* out) {
         d.out_idx = (int)i;
     }
     const int W = pick_W(job.pairs, single);
-    plan(job, W, pick_C(W));
+    plan(job, W, pick_C(W), single);
     if (c->seq.ensure(bytes, s) || c->scores.ensure(act.size(), s) || c->hscores.ensure(act.size())) return -1;
     HIPCHK(hipMemcpyAsync(c->seq.p, c->hseq.p, bytes, hipMemcpyHostToDevice, s));
     if (enqueue(c, job, prm, c->seq.p, c->scores.p, (int)act.size(), s, true)) return -1;
@@ -550,7 +577,7 @@ int sw_score_batch_device(const unsigned char* d_arena, const int64_t* a_off, co
     const bool single = idx.size() == 1;
     for (size_t i = 0; i < idx.size(); ++i) {
         const int k = idx[i];
-        bool swap = single ? (blen[k] > alen[k]) : (alen[k] > blen[k]);
+        const bool swap = want_swap(single, alen[k], blen[k]);
         PairDesc& d = job.pairs[i];
         d.col_off = (uint64_t)(swap ? b_off[k] : a_off[k]);
         d.row_off = (uint64_t)(swap ? a_off[k] : b_off[k]);
@@ -564,7 +591,7 @@ int sw_score_batch_device(const unsigned char* d_arena, const int64_t* a_off, co
         return 0;
     }
     const int W = pick_W(job.pairs, single);
-    plan(job, W, pick_C(W));
+    plan(job, W, pick_C(W), single);
     if (flags & SW_FLAG_BYTES || g_opt_bytes.load()) {
         job.dna = false;
     } else if (flags & SW_FLAG_DNA) {
@@ -623,6 +650,12 @@ int sw_set_option(const char* key, long long v) {
     } else if (k == "blocks") {
         if (v < 0) return -1;
         g_opt_blocks = v;
+    } else if (k == "orient") {
+        if (v < 0 || v > 2) return -1;
+        g_opt_orient = v;
+    } else if (k == "mode") {
+        if (v < -1 || v > 2) return -1;
+        g_opt_mode = v;
     } else {
         set_err("unknown option '%s'", key);
         return -1;
@@ -638,6 +671,8 @@ long long sw_get_option(const char* key) {
     if (k == "bytes") return g_opt_bytes;
     if (k == "timeout") return g_opt_timeout;
     if (k == "blocks") return g_opt_blocks;
+    if (k == "orient") return g_opt_orient;
+    if (k == "mode") return g_opt_mode;
     return -1;
 }
 

@@ -59,12 +59,19 @@ struct KParams {
     long long timeout_ticks;      // s_memrealtime ticks (100 MHz) before a spin gives up
 };
 
+// Grid organisations (sw_kernels.hip):
+//   MODE_STRIP  independent waves claim (pair, strip) items in order
+//   MODE_PAIRWG one workgroup per pair, its 4 waves interleave the strips
+//   MODE_CHAIN  one workgroup per group of 4 consecutive strips, LDS hand-offs
+enum : int { MODE_STRIP = 0, MODE_PAIRWG = 1, MODE_CHAIN = 2 };
+
 // Host-side launch (sw_kernels.hip).
 struct LaunchCfg {
     int W;          // columns per lane
     int C;          // rows per hand-off chunk
     bool dna;       // 2-bit ACGT profile path (else raw-byte compare)
-    int blocks;     // persistent workgroups (256 threads = 4 independent waves)
+    int blocks;     // persistent workgroups (256 threads = 4 waves)
+    int mode;       // MODE_*
 };
 
 hipError_t launch_sw_strip(const LaunchCfg& cfg, const KParams& kp, hipStream_t stream);

@@ -17,7 +17,7 @@
 //     comes from E or F is <= some earlier H (penalties >= 0), so max H ==
 //     max(0, max t).
 //
-// Work decomposition (Kernel):
+// Work decomposition (Kernels):
 //   * a WAVE owns a strip of 64*W consecutive columns; lane l holds columns
 //     [l*W, l*W+W) of the strip in registers;
 //   * the wave sweeps the strip's rows as an anti-diagonal wavefront: at step k
@@ -26,15 +26,24 @@
 //     0 is the previous step's position W-1 of lane l-1: ONE wave_shr:1 DPP
 //     move per flowing quantity (H-G_INIT, E-G_EXT, row code) per step;
 //   * the strip's left column enters at lane 0 and its right column leaves at
-//     lane 63 through one "combined" register per quantity that is rotated by
-//     wave_shl:1 every step (lane 0 consumes the next inflow, lane 63 collects
-//     the outflow), so C rows of hand-off cost one 16-byte load and one
-//     16-byte store per lane per C steps;
-//   * strips hand off through tagged 16-byte granules (write-through sc1
-//     stores, sc1 polls; no fences), and waves claim (pair, strip) items
-//     strictly in order from one atomic counter, so a consumer's producer has
-//     always been claimed by a running wave: no co-residency assumption, no
-//     deadlock, any grid size.
+//     lane 63 through one I/O register per quantity that is rotated by
+//     wave_rol:1 every step (lane 0 consumes the next inflow, lane 63 collects
+//     the outflow), so C rows of hand-off cost one load and one store per lane;
+//   * three grid organisations share that strip pass:
+//       sw_strip_kernel  -- independent waves claim (pair, strip) items in
+//                           order; strips hand off through tagged granules;
+//       sw_chain_kernel  -- a single long pair: a workgroup's 4 waves run 4
+//                           consecutive strips in lock step (barrier per
+//                           chunk) with LDS-ring hand-offs, granules only
+//                           between workgroups;
+//       sw_pairwg_kernel -- batches: a workgroup's 4 waves interleave one
+//                           pair's strips (wave w: strips w, w+4, ...), so
+//                           every granule hand-off has a whole strip pass of
+//                           slack and all 4 chains are co-resident.
+//   * strip boundaries cross CUs as tagged 16-byte granules (write-through sc1
+//     stores, sc1 polls; no fences); work is claimed strictly in order or
+//     assigned so that every producer is resident: no co-residency assumption
+//     beyond the workgroup, no deadlock, any grid size.
 #include "sw_internal.h"
 
 namespace swmi {
@@ -43,7 +52,7 @@ namespace {
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int DPP_WAVE_SHL1 = 0x130;
+constexpr int DPP_WAVE_ROL1 = 0x134;
 constexpr int DPP_WAVE_SHR1 = 0x138;
 constexpr unsigned RSRC_FLAGS = 0x00020000u;   // raw buffer, gfx950 (cdna_hip_programming.md T8)
 constexpr int AUX_SC1 = 16;                    // cache policy: sc1 (L1 bypass / write-through)
@@ -57,10 +66,19 @@ constexpr int DEAD = 1 << 29;          // t offset that keeps dead columns out o
 __device__ __forceinline__ int dpp_shr1(int old, int src) {
     return __builtin_amdgcn_update_dpp(old, src, DPP_WAVE_SHR1, 0xF, 0xF, false);
 }
-__device__ __forceinline__ int dpp_shl1(int old, int src) {
-    return __builtin_amdgcn_update_dpp(old, src, DPP_WAVE_SHL1, 0xF, 0xF, false);
+__device__ __forceinline__ int dpp_rol1(int src) {   // every lane has a source: no 'old', no copy
+    return __builtin_amdgcn_mov_dpp(src, DPP_WAVE_ROL1, 0xF, 0xF, true);
 }
 __device__ __forceinline__ int max3i(int a, int b, int c) { return max(max(a, b), c); }
+// v_max3_i32 the compiler cannot split: when it knows two operands are >= 0 it
+// emits v_max_i32 + v_max_u32 instead.  A plain VOP3 (hardware interlocked);
+// every consumer of the result is compiler-visible, so DPP wait states after it
+// are still inserted by the compiler.
+__device__ __forceinline__ int vmax3(int a, int b, int c) {
+    int d;
+    asm("v_max3_i32 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+    return d;
+}
 __device__ __forceinline__ uint64_t uniform64(uint64_t v) {
     const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v);
     const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
@@ -70,191 +88,242 @@ __device__ __forceinline__ uint64_t uniform64(uint64_t v) {
 // 'A','C','G','T' -> 0,1,2,3  (only used when the host verified the alphabet)
 __device__ __forceinline__ int dna_code(unsigned c) { return (int)(((c >> 1) ^ (c >> 2)) & 3u); }
 
-// One anti-diagonal step for the W positions of a lane.
-//   hgCur : on entry H-G_INIT two steps ago (diagonal source); on exit this step's
-//   hgPrev: H-G_INIT of the previous step (left source for p>0, up source for F)
-//   eh, r : E-G_EXT and row code of the previous step, updated in place
-//   fh    : F-G_EXT of the previous step (own column), updated in place
-// Positions are processed from W-1 down to 0 so that the in-place arrays still
-// hold the previous step's value of p-1 when position p reads it.
-template <int W, bool DNA>
-__device__ __forceinline__ void sw_step(int (&hgCur)[W], const int (&hgPrev)[W], int (&eh)[W], int (&r)[W],
-                                        int (&fh)[W], const int (&prof)[W], const int (&tb)[W], int& L0,
-                                        int& IOH, int& IOE, int& IOR, int& M, const int go, const int ge,
-                                        const int ma, const int mi) {
-    const int hgL0 = dpp_shr1(IOH, hgPrev[W - 1]);
-    const int ehL0 = dpp_shr1(IOE, eh[W - 1]);
-    const int rL0 = dpp_shr1(IOR, r[W - 1]);
-#pragma unroll
-    for (int p = W - 1; p >= 0; --p) {
-        const int q = p > 0 ? p - 1 : 0;
-        const int hgL = p > 0 ? hgPrev[q] : hgL0;
-        const int ehL = p > 0 ? eh[q] : ehL0;
-        const int rL = p > 0 ? r[q] : rL0;
-        const int hgD = p > 0 ? hgCur[q] : L0;
-        int s;
-        if constexpr (DNA) {
-            s = (int)__builtin_amdgcn_perm(0u, (unsigned)prof[p], (unsigned)rL);   // biased byte
-        } else {
-            s = (rL == prof[p]) ? ma : mi;
-        }
-        const int t = hgD + s + tb[p];                 // H[i-1][j-1] + s(q_j, d_i)   (v_add3_u32)
-        const int E = max3i(ehL, hgL, 0);              // clamped E
-        const int F = max3i(fh[p], hgPrev[p], 0);      // clamped F
-        const int H = max3i(t, E, F);
-        M = max(M, t);
-        hgCur[p] = H - go;
-        eh[p] = E - ge;
-        fh[p] = F - ge;
-        r[p] = rL;
-    }
-    L0 = hgL0;
-    IOH = dpp_shl1(hgCur[W - 1], IOH);   // lane 63 <- this step's right-edge output
-    IOE = dpp_shl1(eh[W - 1], IOE);
-    IOR = dpp_shl1(IOR, IOR);
+__device__ __forceinline__ PairDesc load_pair(const KParams& kp, int idx) {
+    // every field made provably wave-uniform: buffer descriptors built from them
+    // must live in SGPRs (no waterfall loops, cdna_hip_programming.md T20)
+    const PairDesc raw = kp.pairs[idx];
+    PairDesc pd;
+    pd.col_off = uniform64(raw.col_off);
+    pd.row_off = uniform64(raw.row_off);
+    pd.bnd_off = uniform64(raw.bnd_off);
+    pd.n = __builtin_amdgcn_readfirstlane(raw.n);
+    pd.m = __builtin_amdgcn_readfirstlane(raw.m);
+    pd.strips = __builtin_amdgcn_readfirstlane(raw.strips);
+    pd.out_idx = __builtin_amdgcn_readfirstlane(raw.out_idx);
+    return pd;
 }
 
-struct RowFetch {
-    int code;
-    u32x4 g;
-};
-
-template <int W, int C, bool DNA>
-__device__ __forceinline__ RowFetch fetch_rows(const __amdgpu_buffer_rsrc_t row_rsrc, const __amdgpu_buffer_rsrc_t in_rsrc,
-                                               bool has_in, int k0, int lane, int m) {
-    RowFetch f;
-    const int row = k0 + lane;
-    const bool live = lane < C && row < m;
-    const unsigned ch = __builtin_amdgcn_raw_buffer_load_b8(row_rsrc, live ? (unsigned)row : OOR, 0, 0);
-    if constexpr (DNA) f.code = live ? (dna_code(ch) | 0x0C0C0C00) : SENT_DNA;
-    else f.code = live ? (int)ch : SENT_BYTE;
-    if (has_in) {
-        f.g = __builtin_amdgcn_raw_buffer_load_b128(in_rsrc, live ? (unsigned)row * 16u : OOR, 0, AUX_SC1);
-    } else {
-        f.g = u32x4{0u, 0u, 0u, 0u};
+// last pair whose item_base <= item (uniform binary search)
+__device__ __forceinline__ int find_pair(const KParams& kp, int item) {
+    int lo = 0, hi = kp.npairs - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (kp.item_base[mid] <= item) lo = mid; else hi = mid - 1;
     }
-    return f;
+    return __builtin_amdgcn_readfirstlane(lo);
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t bnd_rsrc(const KParams& kp, const PairDesc& pd, int boundary) {
+    Granule* base = kp.bnd + pd.bnd_off + (uint64_t)(boundary < 0 ? 0 : boundary) * (uint64_t)pd.m;
+    return __builtin_amdgcn_make_buffer_rsrc(base, 0, pd.m * 16, RSRC_FLAGS);
 }
 
 __device__ __forceinline__ bool granule_ok(const u32x4& g, unsigned epoch, int row) {
     return g.x == epoch && g.w == granule_chk(epoch, (int)g.y, (int)g.z, row);
 }
 
-template <int W, int C, bool DNA>
-__device__ void sw_item(const KParams& kp, const PairDesc& pd, const int strip, const int lane) {
-    constexpr int SW = 64 * W;
-    static_assert(C % 4 == 0 && C <= 64, "chunk");
-    const int n = pd.n, m = pd.m;
-    const int go = kp.gap_init, ge = kp.gap_ext, ma = kp.match, mi = kp.mismatch;
-    const unsigned epoch = kp.epoch;
-    const unsigned char* colseq = kp.seq + pd.col_off;
+// ---------------------------------------------------------------------------
+// Per-lane state of one strip pass (W columns per lane).
+// ---------------------------------------------------------------------------
+template <int W, bool DNA>
+struct Strip {
+    int prof[W], tb[W];                     // column profile / bias (fixed for the strip)
+    int hgA[W], hgB[W], eh[W], r[W], fh[W]; // DP state, see step()
+    int L0, M, IOH, IOE, IOR;
 
-    // ---- column state (fixed for the strip) --------------------------------
-    int prof[W], tb[W];
+    __device__ __forceinline__ void setup(const KParams& kp, const PairDesc& pd, int strip, int lane) {
+        constexpr int SW = 64 * W;
+        const int go = kp.gap_init, ge = kp.gap_ext;
+        const unsigned char* colseq = kp.seq + pd.col_off;
 #pragma unroll
-    for (int p = 0; p < W; ++p) {
-        const int c = strip * SW + lane * W + p;
-        if (c < n) {
-            const unsigned ch = colseq[c];
-            if constexpr (DNA) {
-                const int code = dna_code(ch);
-                const unsigned pw = code == 0 ? kp.prof[0] : code == 1 ? kp.prof[1] : code == 2 ? kp.prof[2] : kp.prof[3];
-                prof[p] = (int)pw;
-                tb[p] = go - 128;
+        for (int p = 0; p < W; ++p) {
+            const int c = strip * SW + lane * W + p;
+            if (c < pd.n) {
+                const unsigned ch = colseq[c];
+                if constexpr (DNA) {
+                    const int code = dna_code(ch);
+                    prof[p] = (int)(code == 0 ? kp.prof[0] : code == 1 ? kp.prof[1] : code == 2 ? kp.prof[2] : kp.prof[3]);
+                    tb[p] = go - 128;
+                } else {
+                    prof[p] = (int)ch;
+                    tb[p] = go;
+                }
             } else {
-                prof[p] = (int)ch;
-                tb[p] = go;
+                prof[p] = DNA ? 0 : DEAD_COL_BYTE;
+                tb[p] = -DEAD;
             }
-        } else {
-            prof[p] = DNA ? 0 : DEAD_COL_BYTE;
-            tb[p] = -DEAD;
+        }
+        const int sent = DNA ? SENT_DNA : SENT_BYTE;
+#pragma unroll
+        for (int p = 0; p < W; ++p) {   // everything starts at the border (H = E = F = 0)
+            hgA[p] = -go; hgB[p] = -go; eh[p] = -ge; fh[p] = -ge; r[p] = sent;
+        }
+        L0 = -go; M = 0; IOH = -go; IOE = -ge; IOR = sent;
+    }
+
+    // One anti-diagonal step for the W positions of the lane.
+    //   hgCur : on entry H-G_INIT two steps ago (diagonal source); on exit this step's
+    //   hgPrev: H-G_INIT of the previous step (left source for p>0, up source for F)
+    //   eh, r : E-G_EXT and row code of the previous step, updated in place
+    //   fh    : F-G_EXT of the previous step (own column), updated in place
+    // Positions run from W-1 down to 0 so the in-place arrays still hold the
+    // previous step's p-1 when p reads it.  The I/O registers are rotated first so
+    // the inflow DPPs can take them as their (dying) 'old' operand: no copies.
+    __device__ __forceinline__ void step(int (&hgCur)[W], const int (&hgPrev)[W], const bool l63, const int go,
+                                         const int ge, const int ma, const int mi) {
+        const int ioh = dpp_rol1(IOH), ioe = dpp_rol1(IOE), ior = dpp_rol1(IOR);
+        const int hgL0 = dpp_shr1(IOH, hgPrev[W - 1]);
+        const int ehL0 = dpp_shr1(IOE, eh[W - 1]);
+        const int rL0 = dpp_shr1(IOR, r[W - 1]);
+#pragma unroll
+        for (int p = W - 1; p >= 0; --p) {
+            const int q = p > 0 ? p - 1 : 0;
+            const int hgL = p > 0 ? hgPrev[q] : hgL0;
+            const int ehL = p > 0 ? eh[q] : ehL0;
+            const int rL = p > 0 ? r[q] : rL0;
+            const int hgD = p > 0 ? hgCur[q] : L0;
+            int s;
+            if constexpr (DNA) {
+                s = (int)__builtin_amdgcn_perm(0u, (unsigned)prof[p], (unsigned)rL);   // biased byte
+            } else {
+                s = (rL == prof[p]) ? ma : mi;
+            }
+            const int t = hgD + s + tb[p];               // H[i-1][j-1] + s(q_j, d_i)   (v_add3_u32)
+            const int E = max3i(ehL, hgL, 0);            // clamped E
+            const int F = max3i(fh[p], hgPrev[p], 0);    // clamped F
+            const int H = vmax3(t, E, F);
+            M = max(M, t);
+            hgCur[p] = H - go;
+            eh[p] = E - ge;
+            fh[p] = F - ge;
+            r[p] = rL;
+        }
+        L0 = hgL0;
+        IOH = l63 ? hgCur[W - 1] : ioh;   // lane 63 <- this step's right-edge output
+        IOE = l63 ? eh[W - 1] : ioe;
+        IOR = ior;
+    }
+
+    template <int C>
+    __device__ __forceinline__ void run(const bool l63, const int go, const int ge, const int ma, const int mi) {
+#pragma unroll 2
+        for (int s = 0; s < C; s += 2) {
+            step(hgA, hgB, l63, go, ge, ma, mi);
+            step(hgB, hgA, l63, go, ge, ma, mi);
         }
     }
 
-    // ---- DP state: everything starts at the border (H = E = F = 0) --------
-    int hgA[W], hgB[W], eh[W], r[W], fh[W];
-    const int sent = DNA ? SENT_DNA : SENT_BYTE;
-#pragma unroll
-    for (int p = 0; p < W; ++p) {
-        hgA[p] = -go; hgB[p] = -go; eh[p] = -ge; fh[p] = -ge; r[p] = sent;
+    // inflow of the next C rows into lanes [0, C)
+    __device__ __forceinline__ void feed(int lane, int C, int hg_in, int eh_in, int code) {
+        if (lane < C) { IOH = hg_in; IOE = eh_in; IOR = code; }
     }
-    int L0 = -go, M = 0;
-    int IOH = -go, IOE = -ge, IOR = sent;
+
+    __device__ __forceinline__ void commit_max(const KParams& kp, const PairDesc& pd, int lane) {
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) M = max(M, __shfl_xor(M, off));
+        if (lane == 0 && M > 0) atomicMax(&kp.scores[pd.out_idx], M);
+    }
+};
+
+// Row codes of rows [k0, k0+C) for lanes [0, C); sentinel outside [0, m).
+template <int C, bool DNA>
+__device__ __forceinline__ int fetch_codes(const __amdgpu_buffer_rsrc_t row_rsrc, int k0, int lane, int m) {
+    const int row = k0 + lane;
+    const bool live = lane < C && row >= 0 && row < m;
+    const unsigned ch = __builtin_amdgcn_raw_buffer_load_b8(row_rsrc, live ? (unsigned)row : OOR, 0, 0);
+    if constexpr (DNA) return live ? (dna_code(ch) | 0x0C0C0C00) : SENT_DNA;
+    else return live ? (int)ch : SENT_BYTE;
+}
+
+template <int C>
+__device__ __forceinline__ u32x4 fetch_granules(const __amdgpu_buffer_rsrc_t in_rsrc, int k0, int lane, int m) {
+    const int row = k0 + lane;
+    const bool live = lane < C && row >= 0 && row < m;
+    return __builtin_amdgcn_raw_buffer_load_b128(in_rsrc, live ? (unsigned)row * 16u : OOR, 0, AUX_SC1);
+}
+
+// Wait until the granules of rows [k0, k0+C) are all published (bounded spin).
+template <int C>
+__device__ __forceinline__ void await_granules(const KParams& kp, const __amdgpu_buffer_rsrc_t in_rsrc, u32x4& g,
+                                               int k0, int lane, int m, int strip, bool& failed) {
+    if (failed) return;
+    const int row = k0 + lane;
+    bool ok = lane >= C || row < 0 || row >= m || granule_ok(g, kp.epoch, row);
+    if (__all(ok)) return;
+    const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+    for (;;) {
+        __builtin_amdgcn_s_sleep(1);
+        if (!ok) g = __builtin_amdgcn_raw_buffer_load_b128(in_rsrc, (unsigned)row * 16u, 0, AUX_SC1);
+        ok = lane >= C || row < 0 || row >= m || granule_ok(g, kp.epoch, row);
+        if (__all(ok)) return;
+        if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > kp.timeout_ticks) {
+            if (lane == 0) {
+                atomicOr(&kp.ctrl->error, ERR_TIMEOUT);
+                atomicMax(&kp.ctrl->err_item, (unsigned)strip);
+            }
+            failed = true;
+            return;
+        }
+    }
+}
+
+// Publish the right-edge outflow collected in lanes [64-C, 64) of a chunk that
+// started at step k0: rows k0 - (64W-1) .. k0 + C - 1 - (64W-1).
+template <int W, int C>
+__device__ __forceinline__ void publish_granules(const KParams& kp, const __amdgpu_buffer_rsrc_t out_rsrc, int k0,
+                                                 int lane, int m, int IOH, int IOE) {
+    const int row_out = k0 + (lane - (64 - C)) - (64 * W - 1);
+    const bool st = lane >= 64 - C && row_out >= 0 && row_out < m;
+    u32x4 g;
+    g.x = kp.epoch;
+    g.y = (unsigned)IOH;
+    g.z = (unsigned)IOE;
+    g.w = granule_chk(kp.epoch, IOH, IOE, row_out);
+    __builtin_amdgcn_raw_buffer_store_b128(g, out_rsrc, st ? (unsigned)row_out * 16u : OOR, 0, AUX_SC1);
+}
+
+// One full strip pass with granule inflow (strip > 0) and outflow (strip < strips-1).
+template <int W, int C, bool DNA>
+__device__ void strip_pass(const KParams& kp, const PairDesc& pd, const int strip, const int lane) {
+    constexpr int SW = 64 * W;
+    static_assert(C % 4 == 0 && C <= 64 && (C & (C - 1)) == 0, "chunk");
+    const int m = pd.m;
+    const int go = kp.gap_init, ge = kp.gap_ext, ma = kp.match, mi = kp.mismatch;
+    const bool l63 = lane == 63;
+    Strip<W, DNA> S;
+    S.setup(kp, pd, strip, lane);
 
     const bool has_in = strip > 0;
     const bool has_out = strip < pd.strips - 1;
-    Granule* in_base = kp.bnd + pd.bnd_off + (uint64_t)(has_in ? strip - 1 : 0) * (uint64_t)m;
-    Granule* out_base = kp.bnd + pd.bnd_off + (uint64_t)strip * (uint64_t)m;
-    const __amdgpu_buffer_rsrc_t in_rsrc = __builtin_amdgcn_make_buffer_rsrc(in_base, 0, m * 16, RSRC_FLAGS);
-    const __amdgpu_buffer_rsrc_t out_rsrc = __builtin_amdgcn_make_buffer_rsrc(out_base, 0, m * 16, RSRC_FLAGS);
+    const __amdgpu_buffer_rsrc_t in_rsrc = bnd_rsrc(kp, pd, strip - 1);
+    const __amdgpu_buffer_rsrc_t out_rsrc = bnd_rsrc(kp, pd, strip);
     const __amdgpu_buffer_rsrc_t row_rsrc =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned char*>(kp.seq + pd.row_off), 0, m, RSRC_FLAGS);
 
-    const int total_steps = m + SW - 1;
-    const int nchunks = (total_steps + C - 1) / C;
+    const int nchunks = (m + SW - 1 + C - 1) / C;
     bool failed = false;
-
-    RowFetch nxt = fetch_rows<W, C, DNA>(row_rsrc, in_rsrc, has_in, 0, lane, m);
+    int code_nxt = fetch_codes<C, DNA>(row_rsrc, 0, lane, m);
+    u32x4 g_nxt = has_in ? fetch_granules<C>(in_rsrc, 0, lane, m) : u32x4{0u, 0u, 0u, 0u};
     for (int c = 0; c < nchunks; ++c) {
         const int k0 = c * C;
-        RowFetch cur = nxt;
-        const int row = k0 + lane;
-        if (has_in && !failed) {
-            bool ok = lane >= C || row >= m || granule_ok(cur.g, epoch, row);
-            if (!__all(ok)) {
-                const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
-                for (;;) {
-                    __builtin_amdgcn_s_sleep(1);
-                    if (!ok) cur.g = __builtin_amdgcn_raw_buffer_load_b128(in_rsrc, (unsigned)row * 16u, 0, AUX_SC1);
-                    ok = lane >= C || row >= m || granule_ok(cur.g, epoch, row);
-                    if (__all(ok)) break;
-                    if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > kp.timeout_ticks) {
-                        if (lane == 0) {
-                            atomicOr(&kp.ctrl->error, ERR_TIMEOUT);
-                            atomicMax(&kp.ctrl->err_item, (unsigned)strip);
-                        }
-                        failed = true;
-                        break;
-                    }
-                }
-            }
+        const int code = code_nxt;
+        u32x4 g = g_nxt;
+        if (has_in) await_granules<C>(kp, in_rsrc, g, k0, lane, m, strip, failed);
+        if (c + 1 < nchunks) {   // next chunk's rows in flight while this chunk computes
+            code_nxt = fetch_codes<C, DNA>(row_rsrc, k0 + C, lane, m);
+            if (has_in) g_nxt = fetch_granules<C>(in_rsrc, k0 + C, lane, m);
         }
-        // next chunk's rows in flight while this chunk computes
-        if (c + 1 < nchunks) nxt = fetch_rows<W, C, DNA>(row_rsrc, in_rsrc, has_in, k0 + C, lane, m);
-
-        if (lane < C) {
-            const bool real = has_in && row < m;
-            IOH = real ? (int)cur.g.y : -go;
-            IOE = real ? (int)cur.g.z : -ge;
-            IOR = cur.code;
-        }
-
-#pragma unroll 2
-        for (int s = 0; s < C; s += 2) {
-            sw_step<W, DNA>(hgA, hgB, eh, r, fh, prof, tb, L0, IOH, IOE, IOR, M, go, ge, ma, mi);
-            sw_step<W, DNA>(hgB, hgA, eh, r, fh, prof, tb, L0, IOH, IOE, IOR, M, go, ge, ma, mi);
-        }
-
-        if (has_out) {
-            // lanes [64-C, 64) hold the right-edge (H-G_INIT, E-G_EXT) of steps k0..k0+C-1,
-            // i.e. rows k - (SW-1).
-            const int row_out = k0 + (lane - (64 - C)) - (SW - 1);
-            const bool st = lane >= 64 - C && row_out >= 0 && row_out < m;
-            u32x4 g;
-            g.x = epoch;
-            g.y = (unsigned)IOH;
-            g.z = (unsigned)IOE;
-            g.w = granule_chk(epoch, IOH, IOE, row_out);
-            __builtin_amdgcn_raw_buffer_store_b128(g, out_rsrc, st ? (unsigned)row_out * 16u : OOR, 0, AUX_SC1);
-        }
+        const bool real = has_in && k0 + lane < m;
+        S.feed(lane, C, real ? (int)g.y : -go, real ? (int)g.z : -ge, code);
+        S.template run<C>(l63, go, ge, ma, mi);
+        if (has_out) publish_granules<W, C>(kp, out_rsrc, k0, lane, m, S.IOH, S.IOE);
     }
-
-    // wave max, then one device-scope atomic per (pair, strip)
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) M = max(M, __shfl_xor(M, off));
-    if (lane == 0 && M > 0) atomicMax(&kp.scores[pd.out_idx], M);
+    S.commit_max(kp, pd, lane);
 }
 
+// ---------------------------------------------------------------------------
+// Kernel 1: independent waves claim (pair, strip) items strictly in order.
+// ---------------------------------------------------------------------------
 template <int W, int C, bool DNA>
 __global__ void __launch_bounds__(256) sw_strip_kernel(KParams kp) {
     const int lane = threadIdx.x & 63;
@@ -263,39 +332,137 @@ __global__ void __launch_bounds__(256) sw_strip_kernel(KParams kp) {
         if (lane == 0) item = atomicAdd(&kp.ctrl->next_item, 1u);
         item = __builtin_amdgcn_readfirstlane(item);
         if ((int)item >= kp.total_items) return;
-        int lo = 0, hi = kp.npairs - 1;   // last pair with item_base <= item
-        while (lo < hi) {
-            const int mid = (lo + hi + 1) >> 1;
-            if (kp.item_base[mid] <= (int)item) lo = mid; else hi = mid - 1;
-        }
-        // every field made provably wave-uniform: the buffer descriptors built
-        // from them must live in SGPRs (no waterfall loops, guide T20)
-        const PairDesc raw = kp.pairs[lo];
-        PairDesc pd;
-        pd.col_off = uniform64(raw.col_off);
-        pd.row_off = uniform64(raw.row_off);
-        pd.bnd_off = uniform64(raw.bnd_off);
-        pd.n = __builtin_amdgcn_readfirstlane(raw.n);
-        pd.m = __builtin_amdgcn_readfirstlane(raw.m);
-        pd.strips = __builtin_amdgcn_readfirstlane(raw.strips);
-        pd.out_idx = __builtin_amdgcn_readfirstlane(raw.out_idx);
-        const int strip = __builtin_amdgcn_readfirstlane((int)item - kp.item_base[lo]);
-        sw_item<W, C, DNA>(kp, pd, strip, lane);
+        const int pi = find_pair(kp, (int)item);
+        const PairDesc pd = load_pair(kp, pi);
+        const int strip = __builtin_amdgcn_readfirstlane((int)item - kp.item_base[pi]);
+        strip_pass<W, C, DNA>(kp, pd, strip, lane);
     }
+}
+
+// ---------------------------------------------------------------------------
+// Kernel 2 (batches): workgroup b scores pairs b, b+gridDim, ...; its wave w
+// runs strips w, w+4, w+8, ... of each pair.  A consumer wave starts its strip
+// one strip pass after its previous one, so every hand-off but the first of a
+// pair has a full pass of slack.  The four chains of a pair live in one
+// workgroup, hence are co-resident: no deadlock for any grid size.
+// ---------------------------------------------------------------------------
+template <int W, int C, bool DNA>
+__global__ void __launch_bounds__(256) sw_pairwg_kernel(KParams kp) {
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    for (int pi = blockIdx.x; pi < kp.npairs; pi += gridDim.x) {
+        const PairDesc pd = load_pair(kp, pi);
+        for (int strip = wave; strip < pd.strips; strip += 4) strip_pass<W, C, DNA>(kp, pd, strip, lane);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Kernel 3 (one long pair): a workgroup claims a group of 4 consecutive
+// strips; wave w runs strip 4g+w.  The four waves advance in lock step, one
+// barrier per chunk of C rows; wave w+1 runs D = 64W/C + 1 chunks behind wave
+// w and takes its inflow from an LDS ring that wave w filled before the
+// previous barrier (no memory round trip).  Only the group's first and last
+// strips exchange tagged granules with the neighbouring groups.
+// ---------------------------------------------------------------------------
+template <int W, int C, bool DNA>
+__global__ void __launch_bounds__(256) sw_chain_kernel(KParams kp) {
+    constexpr int SW = 64 * W;
+    constexpr int D = SW / C + 1;          // chunk lag between consecutive waves
+    constexpr int R = 4 * C;               // LDS ring rows per link (> 2C+1 live rows)
+    __shared__ int2 ring[3][R];
+    __shared__ int s_item;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const bool l63 = lane == 63;
+    const int go = kp.gap_init, ge = kp.gap_ext, ma = kp.match, mi = kp.mismatch;
+    for (;;) {
+        if (threadIdx.x == 0) s_item = (int)atomicAdd(&kp.ctrl->next_item, 1u);
+        __syncthreads();
+        const int item = __builtin_amdgcn_readfirstlane(s_item);
+        __syncthreads();
+        if (item >= kp.total_items) return;
+        const int pi = find_pair(kp, item);
+        const PairDesc pd = load_pair(kp, pi);
+        const int m = pd.m;
+        const int group = item - kp.item_base[pi];
+        const int strip = 4 * group + wave;
+        const bool real = strip < pd.strips;
+        Strip<W, DNA> S;
+        S.setup(kp, pd, strip, lane);   // past-the-end strips are all dead columns
+        const bool gin = real && wave == 0 && strip > 0;
+        const bool gout = real && wave == 3 && strip < pd.strips - 1;
+        const bool lin = real && wave > 0;
+        const bool lout = real && wave < 3 && strip + 1 < pd.strips;
+        const __amdgpu_buffer_rsrc_t in_rsrc = bnd_rsrc(kp, pd, strip - 1);
+        const __amdgpu_buffer_rsrc_t out_rsrc = bnd_rsrc(kp, pd, strip);
+        const __amdgpu_buffer_rsrc_t row_rsrc =
+            __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned char*>(kp.seq + pd.row_off), 0, m, RSRC_FLAGS);
+        const int nloc = (m + SW - 1 + C - 1) / C;
+        const int nT = nloc + 3 * D;
+        bool failed = false;
+        int c = -wave * D;   // this wave's local chunk
+        int code_nxt = fetch_codes<C, DNA>(row_rsrc, c * C, lane, m);
+        u32x4 g_nxt = gin ? fetch_granules<C>(in_rsrc, c * C, lane, m) : u32x4{0u, 0u, 0u, 0u};
+        for (int T = 0; T < nT; ++T, ++c) {
+            const int k0 = c * C;
+            const bool active = c >= 0 && c < nloc;
+            const int code = code_nxt;
+            u32x4 g = g_nxt;
+            if (gin && active) await_granules<C>(kp, in_rsrc, g, k0, lane, m, strip, failed);
+            code_nxt = fetch_codes<C, DNA>(row_rsrc, k0 + C, lane, m);
+            if (gin) g_nxt = fetch_granules<C>(in_rsrc, k0 + C, lane, m);
+            int hg_in = -go, eh_in = -ge;
+            const int row = k0 + lane;
+            if (active && row >= 0 && row < m && lane < C) {
+                if (gin) {
+                    hg_in = (int)g.y; eh_in = (int)g.z;
+                } else if (lin) {
+                    const int2 v = ring[wave - 1][row & (R - 1)];
+                    hg_in = v.x; eh_in = v.y;
+                }
+            }
+            S.feed(lane, C, hg_in, eh_in, code);
+            S.template run<C>(l63, go, ge, ma, mi);
+            if (active) {
+                if (gout) {
+                    publish_granules<W, C>(kp, out_rsrc, k0, lane, m, S.IOH, S.IOE);
+                } else if (lout) {
+                    const int row_out = k0 + (lane - (64 - C)) - (SW - 1);
+                    if (lane >= 64 - C && row_out >= 0 && row_out < m) ring[wave][row_out & (R - 1)] = make_int2(S.IOH, S.IOE);
+                }
+            }
+            __syncthreads();
+        }
+        if (real) S.commit_max(kp, pd, lane);
+    }
+}
+
+template <class K>
+int occupancy_waves(K kernel) {
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)kernel, 256, 0) != hipSuccess) return 4;
+    return nb * 4;
 }
 
 template <int W, int C, bool DNA>
 hipError_t launch_t(const LaunchCfg& cfg, const KParams& kp, hipStream_t s) {
-    hipLaunchKernelGGL((sw_strip_kernel<W, C, DNA>), dim3(cfg.blocks), dim3(256), 0, s, kp);
+    switch (cfg.mode) {
+        case MODE_STRIP: hipLaunchKernelGGL((sw_strip_kernel<W, C, DNA>), dim3(cfg.blocks), dim3(256), 0, s, kp); break;
+        case MODE_PAIRWG: hipLaunchKernelGGL((sw_pairwg_kernel<W, C, DNA>), dim3(cfg.blocks), dim3(256), 0, s, kp); break;
+        case MODE_CHAIN: hipLaunchKernelGGL((sw_chain_kernel<W, C, DNA>), dim3(cfg.blocks), dim3(256), 0, s, kp); break;
+        default: return hipErrorInvalidValue;
+    }
     return hipGetLastError();
 }
 
 template <int W, int C, bool DNA>
-int waves_t() {
-    int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)sw_strip_kernel<W, C, DNA>, 256, 0) != hipSuccess)
-        return 4;
-    return nb * 4;
+int waves_t(int mode) {
+    switch (mode) {
+        case MODE_STRIP: return occupancy_waves(sw_strip_kernel<W, C, DNA>);
+        case MODE_PAIRWG: return occupancy_waves(sw_pairwg_kernel<W, C, DNA>);
+        case MODE_CHAIN: return occupancy_waves(sw_chain_kernel<W, C, DNA>);
+        default: return 4;
+    }
 }
 
 }  // namespace
@@ -320,7 +487,7 @@ hipError_t launch_sw_strip(const LaunchCfg& cfg, const KParams& kp, hipStream_t 
 
 int kernel_waves_per_cu(const LaunchCfg& cfg) {
 #define SW_OCC(w, c) \
-    if (cfg.W == w && cfg.C == c) return cfg.dna ? waves_t<w, c, true>() : waves_t<w, c, false>();
+    if (cfg.W == w && cfg.C == c) return cfg.dna ? waves_t<w, c, true>(cfg.mode) : waves_t<w, c, false>(cfg.mode);
     SW_VARIANTS(SW_OCC)
 #undef SW_OCC
     return 4;

@@ -89,6 +89,9 @@ int sw_stream_status(void* stream);
  *   "bytes"    1 = force the raw-byte path
  *   "timeout"  seconds before a stalled strip hand-off gives up (default 30)
  *   "blocks"   0 = auto persistent grid, else workgroups per launch
+ *   "orient"   0 = auto, 1 = seq1 spread across lanes, 2 = seq2 across lanes
+ *   "mode"     -1 = auto, 0 = independent strip waves, 1 = workgroup per pair,
+ *              2 = lock-step strip groups (single long pairs)
  * Returns 0, or -1 for an unknown key / bad value. */
 int sw_set_option(const char* key, long long value);
 long long sw_get_option(const char* key);
@@ -100,6 +103,7 @@ typedef struct {
     long long cells;        /* sum of n*m over the launched pairs */
     int W, C, dna, blocks, waves_per_cu, items;
     long long boundary_bytes;
+    int mode;
 } sw_stats;
 int sw_last_stats(sw_stats* out);
 

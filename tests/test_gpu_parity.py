@@ -15,12 +15,14 @@ def _rand_dna(rng, n):
 @pytest.fixture(autouse=True)
 def _defaults(engine):
     engine.set_params(engine.Params())
-    for k in ("W", "C", "bytes", "blocks"):
+    for k in ("W", "C", "bytes", "blocks", "orient"):
         engine.set_option(k, 0)
+    engine.set_option("mode", -1)
     yield
     engine.set_params(engine.Params())
-    for k in ("W", "C", "bytes", "blocks"):
+    for k in ("W", "C", "bytes", "blocks", "orient"):
         engine.set_option(k, 0)
+    engine.set_option("mode", -1)
 
 
 def test_kats_every_entry_point(engine, golden):
@@ -92,6 +94,13 @@ def test_config_c2_single_pair_65536(engine, golden):
     assert engine.SmithWatermanScoreCUDA(a, b) == c["score"] == 7458
     # symmetric: the transposed problem gives the same score
     assert engine.SmithWatermanScoreCUDA(b, a) == c["score"]
+    # every grid organisation and a wider strip agree at full size
+    for mode in (0, 1, 2):
+        engine.set_option("mode", mode)
+        assert engine.SmithWatermanScoreCUDA(a, b) == c["score"], mode
+    engine.set_option("mode", -1)
+    engine.set_option("W", 4)
+    assert engine.SmithWatermanScoreCUDA(a, b) == c["score"]
 
 
 def test_config_c3_batch_1024(engine, golden):
@@ -125,9 +134,12 @@ def test_every_variant_ragged(engine, oracle_mod):
             engine.set_option("C", C)
             for force_bytes in (0, 1):
                 engine.set_option("bytes", force_bytes)
-                assert engine.score_batch(pairs, prm) == exp, (W, C, force_bytes, prm)
-                for (a, b), e in list(zip(pairs, exp))[::4]:
-                    assert engine.score(a, b, prm) == e, (W, C, force_bytes, len(a), len(b))
+                for mode in (0, 1, 2):   # independent strips, workgroup per pair, lock-step chain
+                    engine.set_option("mode", mode)
+                    assert engine.score_batch(pairs, prm) == exp, (W, C, force_bytes, mode, prm)
+                    for (a, b), e in list(zip(pairs, exp))[::4]:
+                        assert engine.score(a, b, prm) == e, (W, C, force_bytes, mode, len(a), len(b))
+                engine.set_option("mode", -1)
 
 
 def test_edges(engine, oracle_mod):
