@@ -128,6 +128,8 @@ struct Ctx {
     DevBuf<Ctrl> ctrl;
     DevBuf<int> scores;
     DevBuf<unsigned> flag;
+    DevBuf<DuoDesc> duo;
+    PinBuf<DuoDesc> hduo;
     PinBuf<unsigned char> hseq;
     PinBuf<PairDesc> hdesc;
     PinBuf<int> hibase;
@@ -178,6 +180,7 @@ struct Job {
     int W = 1, C = 16;
     int mode = MODE_STRIP;
     bool dna = true;
+    std::vector<DuoDesc> duos;   // MODE_DUO only
 };
 
 bool is_dna_byte(unsigned char c) { return c == 'A' || c == 'C' || c == 'G' || c == 'T'; }
@@ -244,12 +247,72 @@ void plan(Job& job, int W, int C, bool single) {
         PairDesc& d = job.pairs[k];
         d.bnd_off = g;
         g += (uint64_t)(d.strips - 1) * (uint64_t)d.m;
-        const int items = job.mode == MODE_CHAIN ? (d.strips + 3) / 4 : job.mode == MODE_PAIRWG ? 1 : d.strips;
+        const int items = job.mode == MODE_CHAIN ? (d.strips + 3) / 4 : job.mode == MODE_STRIP ? d.strips : 1;
         job.item_base[k + 1] = job.item_base[k] + items;
         cells += (long long)d.n * (long long)d.m;
     }
     job.bnd_granules = g;
     job.cells = cells;
+}
+
+// Packed-u16 duo mode: exact when every H + MATCH fits 16 bits (H <= MATCH*min(n,m)).
+bool duo_fits(const Job& job, const Params& p) {
+    if (!job.dna || p.gap_init + p.match > 65535 || p.gap_ext > 65535 || p.match - p.mismatch > 254) return false;
+    for (auto& d : job.pairs)
+        if ((long long)std::max(p.match, 1) * std::min(d.n, d.m) + p.match > 65535) return false;
+    return true;
+}
+
+// Turn a planned pair list into duos: pairs sorted by shape, neighbours share a
+// duo (padding to the larger shape), boundaries sized by the padded rows.
+void plan_duos(Job& job) {
+    std::vector<int> ord(job.pairs.size());
+    for (size_t i = 0; i < ord.size(); ++i) ord[i] = (int)i;
+    std::sort(ord.begin(), ord.end(), [&](int x, int y) {
+        const PairDesc &a = job.pairs[x], &b = job.pairs[y];
+        return a.n != b.n ? a.n > b.n : a.m > b.m;
+    });
+    job.duos.clear();
+    uint64_t g = 0;
+    for (size_t i = 0; i < ord.size(); i += 2) {
+        const PairDesc& a = job.pairs[ord[i]];
+        const bool two = i + 1 < ord.size();
+        const PairDesc& b = job.pairs[two ? ord[i + 1] : ord[i]];
+        DuoDesc d{};
+        d.col_off[0] = a.col_off; d.row_off[0] = a.row_off; d.n[0] = a.n; d.m[0] = a.m; d.out_idx[0] = a.out_idx;
+        if (two) {
+            d.col_off[1] = b.col_off; d.row_off[1] = b.row_off; d.n[1] = b.n; d.m[1] = b.m; d.out_idx[1] = b.out_idx;
+        } else {
+            d.col_off[1] = a.col_off; d.row_off[1] = a.row_off; d.n[1] = 0; d.m[1] = 0; d.out_idx[1] = -1;
+        }
+        d.n_pad = std::max(d.n[0], d.n[1]);
+        d.m_pad = std::max(d.m[0], d.m[1]);
+        d.strips = (d.n_pad + 64 * job.W - 1) / (64 * job.W);
+        d.bnd_off = g;
+        g += (uint64_t)(d.strips - 1) * (uint64_t)d.m_pad;
+        job.duos.push_back(d);
+    }
+    job.bnd_granules = g;
+    job.item_base.assign(job.duos.size() + 1, 0);
+    for (size_t k = 0; k < job.duos.size(); ++k) job.item_base[k + 1] = (int)(k + 1);
+}
+
+// After the alphabet is known: promote an automatic pair-per-workgroup plan to
+// the packed duo kernel when it is exact, or honour a forced duo request.
+int finalize_mode(Job& job, const Params& prm) {
+    const bool forced_duo = job.mode == MODE_DUO;
+    if (forced_duo || (g_opt_mode.load() < 0 && job.mode == MODE_PAIRWG)) {
+        if (duo_fits(job, prm)) {
+            job.mode = MODE_DUO;
+            plan_duos(job);
+            return 0;
+        }
+        if (forced_duo) {
+            set_err("duo mode needs an {A,C,G,T} batch whose scores fit 16 bits (MATCH*min(n,m)+MATCH <= 65535)");
+            return -1;
+        }
+    }
+    return 0;
 }
 
 void profile_words(const Params& p, unsigned out[4]) {
@@ -280,16 +343,18 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
         set_err("no kernel variant for W=%d C=%d", job.W, job.C);
         return -1;
     }
-    const size_t np = job.pairs.size();
+    const bool duo = job.mode == MODE_DUO;
+    const size_t np = duo ? job.duos.size() : job.pairs.size();
     // staging buffers may still be read by the previous call's async copies
     if (c->staged_pending) {
         HIPCHK(hipEventSynchronize(c->staged));
         c->staged_pending = false;
     }
-    if (c->hdesc.ensure(np) || c->hibase.ensure(np + 1)) return -1;
-    std::memcpy(c->hdesc.p, job.pairs.data(), np * sizeof(PairDesc));
+    if (c->hdesc.ensure(np) || c->hibase.ensure(np + 1) || c->hduo.ensure(np)) return -1;
+    if (duo) std::memcpy(c->hduo.p, job.duos.data(), np * sizeof(DuoDesc));
+    else std::memcpy(c->hdesc.p, job.pairs.data(), np * sizeof(PairDesc));
     std::memcpy(c->hibase.p, job.item_base.data(), (np + 1) * sizeof(int));
-    if (c->desc.ensure(np, s) || c->ibase.ensure(np + 1, s) || c->ctrl.ensure(1, s)) return -1;
+    if (c->desc.ensure(np, s) || c->duo.ensure(np, s) || c->ibase.ensure(np + 1, s) || c->ctrl.ensure(1, s)) return -1;
     if (job.bnd_granules) {
         size_t freeb = 0, totb = 0;
         HIPCHK(hipMemGetInfo(&freeb, &totb));
@@ -300,7 +365,8 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
         }
         if (c->bnd.ensure(job.bnd_granules, s)) return -1;
     }
-    HIPCHK(hipMemcpyAsync(c->desc.p, c->hdesc.p, np * sizeof(PairDesc), hipMemcpyHostToDevice, s));
+    if (duo) HIPCHK(hipMemcpyAsync(c->duo.p, c->hduo.p, np * sizeof(DuoDesc), hipMemcpyHostToDevice, s));
+    else HIPCHK(hipMemcpyAsync(c->desc.p, c->hdesc.p, np * sizeof(PairDesc), hipMemcpyHostToDevice, s));
     HIPCHK(hipMemcpyAsync(c->ibase.p, c->hibase.p, (np + 1) * sizeof(int), hipMemcpyHostToDevice, s));
     HIPCHK(hipEventRecord(c->staged, s));
     c->staged_pending = true;
@@ -315,7 +381,7 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
         const long long cap = (long long)c->cus * std::max(1, wpc / 4);
         // strip mode: 4 independent waves per block; chain: one block per group;
         // pair-per-workgroup: one block per pair (grid-stride over pairs)
-        const long long want = job.mode == MODE_STRIP ? (items + 3) / 4 : job.mode == MODE_CHAIN ? items : (long long)np;
+        const long long want = job.mode == MODE_STRIP ? (items + 3) / 4 : job.mode == MODE_CHAIN ? items : (long long)np;   // pairwg/duo: np workgroups
         blocks = std::min<long long>(want, cap);
     }
     cfg.blocks = (int)std::max<long long>(1, blocks);
@@ -323,6 +389,7 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
     KParams kp{};
     kp.seq = d_seq;
     kp.pairs = c->desc.p;
+    kp.duos = c->duo.p;
     kp.item_base = c->ibase.p;
     kp.bnd = c->bnd.p;
     kp.ctrl = c->ctrl.p;
@@ -336,6 +403,11 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
     kp.gap_init = prm.gap_init;
     kp.gap_ext = prm.gap_ext;
     profile_words(prm, kp.prof);
+    for (int q = 0; q < 4; ++q) {   // duo: penalty bytes MATCH - s(r, q)
+        unsigned w = 0;
+        for (int r = 0; r < 4; ++r) w |= (unsigned)(r == q ? 0 : prm.match - prm.mismatch) << (8 * r);
+        kp.pen[q] = w;
+    }
     kp.timeout_ticks = g_opt_timeout.load() * 100000000LL;   // s_memrealtime: 100 MHz
 
     if (time_kernel) HIPCHK(hipEventRecord(c->ev0, s));
@@ -440,6 +512,7 @@ int score_host(const HostPair* in, int npairs, const Params& prm, int* out) {
     }
     const int W = pick_W(job.pairs, single);
     plan(job, W, pick_C(W), single);
+    if (finalize_mode(job, prm)) return -1;
     if (c->seq.ensure(bytes, s) || c->scores.ensure(act.size(), s) || c->hscores.ensure(act.size())) return -1;
     HIPCHK(hipMemcpyAsync(c->seq.p, c->hseq.p, bytes, hipMemcpyHostToDevice, s));
     if (enqueue(c, job, prm, c->seq.p, c->scores.p, (int)act.size(), s, true)) return -1;
@@ -614,6 +687,7 @@ int sw_score_batch_device(const unsigned char* d_arena, const int64_t* a_off, co
         HIPCHK(hipStreamSynchronize(s));
         job.dna = *hflag == 0;
     }
+    if (finalize_mode(job, prm)) return -1;
     if (enqueue(c, job, prm, d_arena, d_scores, npairs, s, !stream)) return -1;
     if (!stream) {
         if (check_ctrl(c, s)) return -1;
@@ -654,7 +728,7 @@ int sw_set_option(const char* key, long long v) {
         if (v < 0 || v > 2) return -1;
         g_opt_orient = v;
     } else if (k == "mode") {
-        if (v < -1 || v > 2) return -1;
+        if (v < -1 || v > 3) return -1;
         g_opt_mode = v;
     } else {
         set_err("unknown option '%s'", key);

@@ -19,6 +19,19 @@ struct PairDesc {
     int out_idx;        // slot in the score array
 };
 
+// Two pairs scored in lock step by the packed-u16 "duo" kernel: lane values
+// hold pair 0 in the low and pair 1 in the high 16 bits.  Both are padded to
+// (n_pad, m_pad) with dead columns / sentinel rows.
+struct DuoDesc {
+    uint64_t col_off[2];
+    uint64_t row_off[2];
+    uint64_t bnd_off;   // granule offset of the duo's strip-boundary buffers (m_pad rows each)
+    int n[2], m[2];
+    int n_pad, m_pad;
+    int strips;         // ceil(n_pad / (64*W))
+    int out_idx[2];     // out_idx[1] == -1: no second pair
+};
+
 // Per-launch control block (zeroed by hipMemsetAsync before every launch).
 struct Ctrl {
     unsigned int next_item;   // work-claim counter (items claimed strictly in order)
@@ -56,6 +69,8 @@ struct KParams {
     unsigned epoch;               // != 0, unique per launch
     int match, mismatch, gap_init, gap_ext;
     unsigned prof[4];             // DNA mode: per column code, 4 biased score bytes (row code 0..3)
+    unsigned pen[4];              // duo mode: per column code, 4 penalty bytes MATCH - s (row code 0..3)
+    const DuoDesc* duos;          // duo mode: nduos descriptors (npairs counts duos)
     long long timeout_ticks;      // s_memrealtime ticks (100 MHz) before a spin gives up
 };
 
@@ -63,7 +78,8 @@ struct KParams {
 //   MODE_STRIP  independent waves claim (pair, strip) items in order
 //   MODE_PAIRWG one workgroup per pair, its 4 waves interleave the strips
 //   MODE_CHAIN  one workgroup per group of 4 consecutive strips, LDS hand-offs
-enum : int { MODE_STRIP = 0, MODE_PAIRWG = 1, MODE_CHAIN = 2 };
+//   MODE_DUO    one workgroup per two pairs, packed u16 (DNA, small scores)
+enum : int { MODE_STRIP = 0, MODE_PAIRWG = 1, MODE_CHAIN = 2, MODE_DUO = 3 };
 
 // Host-side launch (sw_kernels.hip).
 struct LaunchCfg {

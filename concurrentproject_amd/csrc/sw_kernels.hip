@@ -437,6 +437,207 @@ __global__ void __launch_bounds__(256) sw_chain_kernel(KParams kp) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// Packed-u16 "duo" path (DNA batches whose scores fit 16 bits): every lane
+// value holds the same cell of two pairs, pair 0 in the low and pair 1 in the
+// high half, so each v_pk_* instruction updates two cells.  Saturating
+// (clamped) arithmetic throughout, exact for the same reasons as the int32
+// path (Arithmetic), with
+//   A  = H + MATCH            exact (the host guarantees MATCH*min(n,m)+MATCH <= 65535)
+//   Hg = max(H - G_INIT, 0),  Eh = max(E - G_EXT, 0),  Fh = max(F - G_EXT, 0)
+//   t  = max(A_diag - pen, 0) with pen = MATCH - s(q, d) from one v_perm_b32
+//        over both pairs' 4-byte column profiles (selector 13 -> 0xFF: dead
+//        columns and sentinel rows get penalty 255, which keeps them <= the
+//        true maximum without a separate mask).
+// ---------------------------------------------------------------------------
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ u16x2 as16(unsigned v) { return __builtin_bit_cast(u16x2, v); }
+__device__ __forceinline__ unsigned as32(u16x2 v) { return __builtin_bit_cast(unsigned, v); }
+__device__ __forceinline__ u16x2 vmax2(u16x2 a, u16x2 b) { return __builtin_elementwise_max(a, b); }
+__device__ __forceinline__ u16x2 vsubs2(u16x2 a, u16x2 b) { return __builtin_elementwise_sub_sat(a, b); }
+__device__ __forceinline__ u16x2 splat2(int v) { return u16x2{(unsigned short)v, (unsigned short)v}; }
+
+constexpr unsigned SENT_DUO = 0x0C0D0C0Du;   // selector 13 in both halves -> penalty 0xFF
+
+__device__ __forceinline__ DuoDesc load_duo(const KParams& kp, int idx) {
+    const DuoDesc raw = kp.duos[idx];
+    DuoDesc d;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        d.col_off[h] = uniform64(raw.col_off[h]);
+        d.row_off[h] = uniform64(raw.row_off[h]);
+        d.n[h] = __builtin_amdgcn_readfirstlane(raw.n[h]);
+        d.m[h] = __builtin_amdgcn_readfirstlane(raw.m[h]);
+        d.out_idx[h] = __builtin_amdgcn_readfirstlane(raw.out_idx[h]);
+    }
+    d.bnd_off = uniform64(raw.bnd_off);
+    d.n_pad = __builtin_amdgcn_readfirstlane(raw.n_pad);
+    d.m_pad = __builtin_amdgcn_readfirstlane(raw.m_pad);
+    d.strips = __builtin_amdgcn_readfirstlane(raw.strips);
+    return d;
+}
+
+template <int W>
+struct StripDuo {
+    unsigned pA[W], pB[W];                   // column penalty words: pair 0 (perm src1), pair 1 (perm src0)
+    u16x2 aA[W], aB[W];                      // A = H + MATCH, ping-pong (diagonal source)
+    u16x2 hg[W], eh[W], fh[W];               // saturated H-G_INIT, E-G_EXT, F-G_EXT
+    unsigned r[W];                           // row-code perm selectors
+    u16x2 L0, M;
+    unsigned IOA, IOE, IOR;
+
+    __device__ __forceinline__ void setup(const KParams& kp, const DuoDesc& d, int strip, int lane) {
+        constexpr int SW = 64 * W;
+        const unsigned char* c0 = kp.seq + d.col_off[0];
+        const unsigned char* c1 = kp.seq + d.col_off[1];
+#pragma unroll
+        for (int p = 0; p < W; ++p) {
+            const int c = strip * SW + lane * W + p;
+            unsigned w0 = 0xFFFFFFFFu, w1 = 0xFFFFFFFFu;   // dead column: penalty 255 for every row code
+            if (c < d.n[0]) {
+                const int q = dna_code(c0[c]);
+                w0 = q == 0 ? kp.pen[0] : q == 1 ? kp.pen[1] : q == 2 ? kp.pen[2] : kp.pen[3];
+            }
+            if (c < d.n[1]) {
+                const int q = dna_code(c1[c]);
+                w1 = q == 0 ? kp.pen[0] : q == 1 ? kp.pen[1] : q == 2 ? kp.pen[2] : kp.pen[3];
+            }
+            pA[p] = w0;
+            pB[p] = w1;
+        }
+        const u16x2 ma2 = splat2(kp.match);
+#pragma unroll
+        for (int p = 0; p < W; ++p) {   // border: H = E = F = 0
+            aA[p] = ma2; aB[p] = ma2; hg[p] = splat2(0); eh[p] = splat2(0); fh[p] = splat2(0); r[p] = SENT_DUO;
+        }
+        L0 = ma2; M = splat2(0); IOA = as32(ma2); IOE = 0u; IOR = SENT_DUO;
+    }
+
+    __device__ __forceinline__ void step(u16x2 (&aCur)[W], const u16x2 (&aPrev)[W], const bool l63, const u16x2 go2,
+                                         const u16x2 ge2, const u16x2 ma2, const u16x2 gom2) {
+        const unsigned ioa = (unsigned)dpp_rol1((int)IOA), ioe = (unsigned)dpp_rol1((int)IOE), ior = (unsigned)dpp_rol1((int)IOR);
+        const u16x2 aL0 = as16((unsigned)dpp_shr1((int)IOA, (int)as32(aPrev[W - 1])));
+        const u16x2 ehL0 = as16((unsigned)dpp_shr1((int)IOE, (int)as32(eh[W - 1])));
+        const unsigned rL0 = (unsigned)dpp_shr1((int)IOR, (int)r[W - 1]);
+        const u16x2 hgL0 = vsubs2(aL0, gom2);   // H - G_INIT of the left neighbour, from its A
+#pragma unroll
+        for (int p = W - 1; p >= 0; --p) {
+            const int q = p > 0 ? p - 1 : 0;
+            const u16x2 hgL = p > 0 ? hg[q] : hgL0;
+            const u16x2 ehL = p > 0 ? eh[q] : ehL0;
+            const unsigned rL = p > 0 ? r[q] : rL0;
+            const u16x2 aD = p > 0 ? aCur[q] : L0;
+            const u16x2 pen = as16(__builtin_amdgcn_perm(pB[p], pA[p], rL));
+            const u16x2 t = vsubs2(aD, pen);                 // max(H_diag + s, 0)
+            const u16x2 E = vmax2(ehL, hgL);
+            const u16x2 F = vmax2(fh[p], hg[p]);
+            const u16x2 H = vmax2(vmax2(t, E), F);
+            M = vmax2(M, t);
+            aCur[p] = H + ma2;
+            hg[p] = vsubs2(H, go2);
+            eh[p] = vsubs2(E, ge2);
+            fh[p] = vsubs2(F, ge2);
+            r[p] = rL;
+        }
+        L0 = aL0;
+        IOA = l63 ? as32(aCur[W - 1]) : ioa;
+        IOE = l63 ? as32(eh[W - 1]) : ioe;
+        IOR = ior;
+    }
+
+    template <int C>
+    __device__ __forceinline__ void run(const bool l63, const u16x2 go2, const u16x2 ge2, const u16x2 ma2,
+                                        const u16x2 gom2) {
+#pragma unroll 2
+        for (int s = 0; s < C; s += 2) {
+            step(aA, aB, l63, go2, ge2, ma2, gom2);
+            step(aB, aA, l63, go2, ge2, ma2, gom2);
+        }
+    }
+
+    __device__ __forceinline__ void commit_max(const KParams& kp, const DuoDesc& d, int lane) {
+        int m0 = M.x, m1 = M.y;
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            m0 = max(m0, __shfl_xor(m0, off));
+            m1 = max(m1, __shfl_xor(m1, off));
+        }
+        if (lane == 0) {
+            if (m0 > 0) atomicMax(&kp.scores[d.out_idx[0]], m0);
+            if (m1 > 0 && d.out_idx[1] >= 0) atomicMax(&kp.scores[d.out_idx[1]], m1);
+        }
+    }
+};
+
+template <int C>
+__device__ __forceinline__ unsigned fetch_codes_duo(const __amdgpu_buffer_rsrc_t r0, const __amdgpu_buffer_rsrc_t r1,
+                                                    int k0, int lane, const DuoDesc& d) {
+    const int row = k0 + lane;
+    const bool l0 = lane < C && row >= 0 && row < d.m[0];
+    const bool l1 = lane < C && row >= 0 && row < d.m[1];
+    const unsigned c0 = __builtin_amdgcn_raw_buffer_load_b8(r0, l0 ? (unsigned)row : OOR, 0, 0);
+    const unsigned c1 = __builtin_amdgcn_raw_buffer_load_b8(r1, l1 ? (unsigned)row : OOR, 0, 0);
+    const unsigned s0 = l0 ? (unsigned)dna_code(c0) : 13u;
+    const unsigned s1 = l1 ? (unsigned)dna_code(c1) + 4u : 13u;
+    return 0x0C000C00u | (s1 << 16) | s0;
+}
+
+template <int W, int C>
+__device__ void strip_pass_duo(const KParams& kp, const DuoDesc& d, const int strip, const int lane) {
+    constexpr int SW = 64 * W;
+    const int m = d.m_pad;
+    const bool l63 = lane == 63;
+    const u16x2 go2 = splat2(kp.gap_init), ge2 = splat2(kp.gap_ext), ma2 = splat2(kp.match),
+                gom2 = splat2(kp.gap_init + kp.match);
+    StripDuo<W> S;
+    S.setup(kp, d, strip, lane);
+    const bool has_in = strip > 0;
+    const bool has_out = strip < d.strips - 1;
+    Granule* in_base = kp.bnd + d.bnd_off + (uint64_t)(has_in ? strip - 1 : 0) * (uint64_t)m;
+    Granule* out_base = kp.bnd + d.bnd_off + (uint64_t)strip * (uint64_t)m;
+    const __amdgpu_buffer_rsrc_t in_rsrc = __builtin_amdgcn_make_buffer_rsrc(in_base, 0, m * 16, RSRC_FLAGS);
+    const __amdgpu_buffer_rsrc_t out_rsrc = __builtin_amdgcn_make_buffer_rsrc(out_base, 0, m * 16, RSRC_FLAGS);
+    const __amdgpu_buffer_rsrc_t r0 =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned char*>(kp.seq + d.row_off[0]), 0, d.m[0], RSRC_FLAGS);
+    const __amdgpu_buffer_rsrc_t r1 =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned char*>(kp.seq + d.row_off[1]), 0, d.m[1], RSRC_FLAGS);
+    const int nchunks = (m + SW - 1 + C - 1) / C;
+    bool failed = false;
+    unsigned code_nxt = fetch_codes_duo<C>(r0, r1, 0, lane, d);
+    u32x4 g_nxt = has_in ? fetch_granules<C>(in_rsrc, 0, lane, m) : u32x4{0u, 0u, 0u, 0u};
+    for (int c = 0; c < nchunks; ++c) {
+        const int k0 = c * C;
+        const unsigned code = code_nxt;
+        u32x4 g = g_nxt;
+        if (has_in) await_granules<C>(kp, in_rsrc, g, k0, lane, m, strip, failed);
+        if (c + 1 < nchunks) {
+            code_nxt = fetch_codes_duo<C>(r0, r1, k0 + C, lane, d);
+            if (has_in) g_nxt = fetch_granules<C>(in_rsrc, k0 + C, lane, m);
+        }
+        if (lane < C) {
+            const bool real = has_in && k0 + lane < m;
+            S.IOA = real ? g.y : as32(ma2);
+            S.IOE = real ? g.z : 0u;
+            S.IOR = code;
+        }
+        S.template run<C>(l63, go2, ge2, ma2, gom2);
+        if (has_out) publish_granules<W, C>(kp, out_rsrc, k0, lane, m, (int)S.IOA, (int)S.IOE);
+    }
+    S.commit_max(kp, d, lane);
+}
+
+// Kernel 4 (DNA batches, 16-bit scores): workgroup b scores duos b, b+gridDim,
+// ...; wave w runs strips w, w+4, ... of each duo (as sw_pairwg_kernel).
+template <int W, int C>
+__global__ void __launch_bounds__(256) sw_duo_kernel(KParams kp) {
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    for (int di = blockIdx.x; di < kp.npairs; di += gridDim.x) {
+        const DuoDesc d = load_duo(kp, di);
+        for (int strip = wave; strip < d.strips; strip += 4) strip_pass_duo<W, C>(kp, d, strip, lane);
+    }
+}
+
 template <class K>
 int occupancy_waves(K kernel) {
     int nb = 0;
@@ -450,6 +651,9 @@ hipError_t launch_t(const LaunchCfg& cfg, const KParams& kp, hipStream_t s) {
         case MODE_STRIP: hipLaunchKernelGGL((sw_strip_kernel<W, C, DNA>), dim3(cfg.blocks), dim3(256), 0, s, kp); break;
         case MODE_PAIRWG: hipLaunchKernelGGL((sw_pairwg_kernel<W, C, DNA>), dim3(cfg.blocks), dim3(256), 0, s, kp); break;
         case MODE_CHAIN: hipLaunchKernelGGL((sw_chain_kernel<W, C, DNA>), dim3(cfg.blocks), dim3(256), 0, s, kp); break;
+        case MODE_DUO:
+            if constexpr (DNA) { hipLaunchKernelGGL((sw_duo_kernel<W, C>), dim3(cfg.blocks), dim3(256), 0, s, kp); break; }
+            return hipErrorInvalidValue;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
@@ -461,6 +665,9 @@ int waves_t(int mode) {
         case MODE_STRIP: return occupancy_waves(sw_strip_kernel<W, C, DNA>);
         case MODE_PAIRWG: return occupancy_waves(sw_pairwg_kernel<W, C, DNA>);
         case MODE_CHAIN: return occupancy_waves(sw_chain_kernel<W, C, DNA>);
+        case MODE_DUO:
+            if constexpr (DNA) return occupancy_waves(sw_duo_kernel<W, C>);
+            return 4;
         default: return 4;
     }
 }

@@ -134,7 +134,8 @@ def test_every_variant_ragged(engine, oracle_mod):
             engine.set_option("C", C)
             for force_bytes in (0, 1):
                 engine.set_option("bytes", force_bytes)
-                for mode in (0, 1, 2):   # independent strips, workgroup per pair, lock-step chain
+                # independent strips, workgroup per pair, lock-step chain, packed u16 duos (DNA only)
+                for mode in ((0, 1, 2) if force_bytes else (0, 1, 2, 3)):
                     engine.set_option("mode", mode)
                     assert engine.score_batch(pairs, prm) == exp, (W, C, force_bytes, mode, prm)
                     for (a, b), e in list(zip(pairs, exp))[::4]:
@@ -200,3 +201,39 @@ def test_errors_are_reported(engine):
     with pytest.raises(engine.SwError):
         engine.score(b"ACGT", b"ACGT", engine.Params(1, -1, -2, 1))   # negative gap
     assert engine.score(b"ACGT", b"ACGT") == 4                       # engine still healthy
+
+
+def test_duo_batches(engine, oracle_mod):
+    """Packed 16-bit duo kernel: odd batch sizes, ragged shapes padded inside a
+    duo, several constants; chosen automatically for DNA batches."""
+    rng = np.random.default_rng(77)
+    for prm in (engine.Params(), engine.Params(2, -3, 5, 2), engine.Params(3, -1, 4, 1)):
+        op = oracle_mod.Params(prm.match, prm.mismatch, prm.gap_init, prm.gap_ext)
+        for npairs in (1, 2, 3, 7):
+            pairs = []
+            for _ in range(npairs):
+                n, m = int(rng.integers(200, 2600)), int(rng.integers(200, 2600))
+                a = _rand_dna(rng, n)
+                b = np.resize(a, m).copy() if rng.random() < 0.5 else _rand_dna(rng, m)
+                mut = rng.random(m) < 0.1
+                b[mut] = _rand_dna(rng, int(mut.sum()))
+                pairs.append((a, b))
+            exp = [oracle_mod.score_linear(a, b, op) for a, b in pairs]
+            engine.set_option("mode", 3)
+            assert engine.score_batch(pairs, prm) == exp, (prm, npairs)
+            engine.set_option("mode", -1)
+            assert engine.score_batch(pairs, prm) == exp, (prm, npairs)
+
+
+def test_duo_16bit_boundary(engine):
+    """H + MATCH must fit 16 bits: 65534 identical bases is the largest exact duo case;
+    one more forces the int32 kernels (auto) or an error (forced duo)."""
+    rng = np.random.default_rng(5)
+    s = _rand_dna(rng, 65535)
+    engine.set_option("mode", 3)
+    pairs = [(s[:65534], s[:65534]), (s[:40000], s[:40000])]
+    assert engine.score_batch(pairs) == [65534, 40000]
+    with pytest.raises(engine.SwError):
+        engine.score_batch([(s, s), (s[:10], s[:10])])
+    engine.set_option("mode", -1)
+    assert engine.score_batch([(s, s), (s[:10], s[:10])]) == [65535, 10]
