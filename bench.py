@@ -95,7 +95,7 @@ def main():
     import torch
     torch.cuda.set_device(local)
     dist = None
-    if world > 1:
+    if world > 1 or "TORCHELASTIC_RUN_ID" in os.environ:   # launched by torch.distributed.run
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     import concurrentproject_amd as sw
@@ -121,10 +121,13 @@ def main():
                "N": N, "pairs_per_gpu": 1, "global_pairs": world,
                "parallelism": "replicas x%d" % world if world > 1 else "single GPU"}
     else:
+        from concurrentproject_amd.dist import shard_bounds
         N = args.n or 8192
         P = args.pairs_per_gpu
-        base = 8192 + rank * P
-        host = sw.gen_batch(base, P, N)
+        lo, hi = shard_bounds(P * world, world, rank)   # contiguous block of the global batch
+        base = 8192 + lo
+        host = sw.gen_batch(base, hi - lo, N)
+        P = hi - lo
         offs_a = [2 * N * k for k in range(P)]
         offs_b = [2 * N * k + N for k in range(P)]
         lens = [N] * P
@@ -138,14 +141,18 @@ def main():
     stream = torch.cuda.current_stream()
     sptr = stream.cuda_stream
     gathered = None
-    if dist is not None and rank == 0:
-        gathered = [torch.zeros_like(scores) for _ in range(world)]
+    total_pairs = npairs_rank * world
+
+    def gather():
+        from concurrentproject_amd.dist import gather_scores
+        return gather_scores(scores, total_pairs)     # RCCL gather of the per-pair int32 scores
 
     def step():
+        nonlocal gathered
         sw.score_batch_device(arena.data_ptr(), offs_a, lens, offs_b, lens, scores.data_ptr(),
                               flags=1, stream=sptr)
         if dist is not None:
-            dist.gather(scores, gathered, dst=0)
+            gathered = gather()
 
     for _ in range(args.warmup):
         step()
@@ -164,7 +171,7 @@ def main():
                               flags=1, stream=sptr)
         ends[i].record(stream)
         if dist is not None:
-            dist.gather(scores, gathered, dst=0)
+            gathered = gather()
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
@@ -191,7 +198,7 @@ def main():
         if workload == "pair" and N == 65536 and world == 1 and "C2" in gold:
             parity = "ok" if scores.cpu().tolist() == [gold["C2"]["score"]] else "MISMATCH"
         elif workload == "batch" and N == 8192:
-            allsc = (torch.cat(gathered).cpu().tolist() if gathered else scores.cpu().tolist())
+            allsc = gathered.cpu().tolist() if gathered is not None else scores.cpu().tolist()
             ref = gold.get("C4", gold.get("C3", {})).get("scores", [])
             if len(ref) >= len(allsc):
                 parity = "ok" if allsc == ref[:len(allsc)] else "MISMATCH"
