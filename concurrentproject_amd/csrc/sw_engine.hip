@@ -246,7 +246,10 @@ void plan(Job& job, int W, int C, bool single) {
     for (size_t k = 0; k < job.pairs.size(); ++k) {
         PairDesc& d = job.pairs[k];
         d.bnd_off = g;
-        g += (uint64_t)(d.strips - 1) * (uint64_t)d.m;
+        // chain mode hands off through LDS inside a group of 4 strips: granule
+        // buffers only between groups; the other modes need one per strip boundary
+        const uint64_t nb = job.mode == MODE_CHAIN ? (uint64_t)((d.strips + 3) / 4 - 1) : (uint64_t)(d.strips - 1);
+        g += nb * (uint64_t)d.m;
         const int items = job.mode == MODE_CHAIN ? (d.strips + 3) / 4 : job.mode == MODE_STRIP ? d.strips : 1;
         job.item_base[k + 1] = job.item_base[k] + items;
         cells += (long long)d.n * (long long)d.m;

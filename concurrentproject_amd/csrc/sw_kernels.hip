@@ -44,6 +44,8 @@
 //     stores, sc1 polls; no fences); work is claimed strictly in order or
 //     assigned so that every producer is resident: no co-residency assumption
 //     beyond the workgroup, no deadlock, any grid size.
+#include <type_traits>
+
 #include "sw_internal.h"
 
 namespace swmi {
@@ -225,14 +227,22 @@ struct Strip {
     }
 };
 
-// Row codes of rows [k0, k0+C) for lanes [0, C); sentinel outside [0, m).
-template <int C, bool DNA>
-__device__ __forceinline__ int fetch_codes(const __amdgpu_buffer_rsrc_t row_rsrc, int k0, int lane, int m) {
+// Row bytes of rows [k0, k0+C) for lanes [0, C), issued one chunk ahead and
+// converted only when the chunk starts (code_of): converting right after the
+// load would make the compiler wait for it (vmcnt(0)) and serialise a memory
+// round trip into every chunk.  Out-of-range lanes load from OOR (returns 0).
+__device__ __forceinline__ unsigned fetch_raw(const __amdgpu_buffer_rsrc_t row_rsrc, int k0, int lane, int C, int m) {
     const int row = k0 + lane;
     const bool live = lane < C && row >= 0 && row < m;
-    const unsigned ch = __builtin_amdgcn_raw_buffer_load_b8(row_rsrc, live ? (unsigned)row : OOR, 0, 0);
-    if constexpr (DNA) return live ? (dna_code(ch) | 0x0C0C0C00) : SENT_DNA;
-    else return live ? (int)ch : SENT_BYTE;
+    return __builtin_amdgcn_raw_buffer_load_b8(row_rsrc, live ? (unsigned)row : OOR, 0, 0);
+}
+
+template <bool DNA>
+__device__ __forceinline__ int code_of(unsigned raw, int k0, int lane, int C, int m) {
+    const int row = k0 + lane;
+    const bool live = lane < C && row >= 0 && row < m;
+    if constexpr (DNA) return live ? (dna_code(raw) | 0x0C0C0C00) : SENT_DNA;
+    else return live ? (int)raw : SENT_BYTE;
 }
 
 template <int C>
@@ -242,29 +252,47 @@ __device__ __forceinline__ u32x4 fetch_granules(const __amdgpu_buffer_rsrc_t in_
     return __builtin_amdgcn_raw_buffer_load_b128(in_rsrc, live ? (unsigned)row * 16u : OOR, 0, AUX_SC1);
 }
 
+// Slow path of await_granules: re-poll until every granule of the chunk is
+// published or the deadline passes.  Out of line on purpose: inlined, its
+// reload loop leaves outstanding loads in the registers of the join point and
+// the compiler then waits for ALL loads (vmcnt(0)) in the fast path, which
+// defeats the one-chunk prefetch.
+struct AwaitRes {
+    u32x4 g;
+    int failed;
+};
+__device__ __noinline__ AwaitRes await_slow(__amdgpu_buffer_rsrc_t in_rsrc, u32x4 g, const int row, const bool need,
+                                            const unsigned epoch, const long long timeout_ticks, Ctrl* ctrl,
+                                            const int strip, const int lane) {
+    const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+    bool ok = !need || granule_ok(g, epoch, row);
+    for (;;) {
+        __builtin_amdgcn_s_sleep(1);
+        if (!ok) g = __builtin_amdgcn_raw_buffer_load_b128(in_rsrc, (unsigned)row * 16u, 0, AUX_SC1);
+        ok = !need || granule_ok(g, epoch, row);
+        if (__all(ok)) return AwaitRes{g, 0};
+        if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > timeout_ticks) {
+            if (lane == 0) {
+                atomicOr(&ctrl->error, ERR_TIMEOUT);
+                atomicMax(&ctrl->err_item, (unsigned)strip);
+            }
+            return AwaitRes{g, 1};
+        }
+    }
+}
+
 // Wait until the granules of rows [k0, k0+C) are all published (bounded spin).
 template <int C>
 __device__ __forceinline__ void await_granules(const KParams& kp, const __amdgpu_buffer_rsrc_t in_rsrc, u32x4& g,
                                                int k0, int lane, int m, int strip, bool& failed) {
     if (failed) return;
     const int row = k0 + lane;
-    bool ok = lane >= C || row < 0 || row >= m || granule_ok(g, kp.epoch, row);
+    const bool need = lane < C && row >= 0 && row < m;
+    const bool ok = !need || granule_ok(g, kp.epoch, row);
     if (__all(ok)) return;
-    const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
-    for (;;) {
-        __builtin_amdgcn_s_sleep(1);
-        if (!ok) g = __builtin_amdgcn_raw_buffer_load_b128(in_rsrc, (unsigned)row * 16u, 0, AUX_SC1);
-        ok = lane >= C || row < 0 || row >= m || granule_ok(g, kp.epoch, row);
-        if (__all(ok)) return;
-        if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > kp.timeout_ticks) {
-            if (lane == 0) {
-                atomicOr(&kp.ctrl->error, ERR_TIMEOUT);
-                atomicMax(&kp.ctrl->err_item, (unsigned)strip);
-            }
-            failed = true;
-            return;
-        }
-    }
+    const AwaitRes r = await_slow(in_rsrc, g, row, need, kp.epoch, kp.timeout_ticks, kp.ctrl, strip, lane);
+    g = r.g;
+    failed = r.failed != 0;
 }
 
 // Publish the right-edge outflow collected in lanes [64-C, 64) of a chunk that
@@ -302,17 +330,17 @@ __device__ void strip_pass(const KParams& kp, const PairDesc& pd, const int stri
 
     const int nchunks = (m + SW - 1 + C - 1) / C;
     bool failed = false;
-    int code_nxt = fetch_codes<C, DNA>(row_rsrc, 0, lane, m);
+    unsigned raw_nxt = fetch_raw(row_rsrc, 0, lane, C, m);
     u32x4 g_nxt = has_in ? fetch_granules<C>(in_rsrc, 0, lane, m) : u32x4{0u, 0u, 0u, 0u};
     for (int c = 0; c < nchunks; ++c) {
         const int k0 = c * C;
-        const int code = code_nxt;
+        const unsigned raw = raw_nxt;
         u32x4 g = g_nxt;
+        // next chunk's rows in flight while this chunk computes
+        raw_nxt = fetch_raw(row_rsrc, k0 + C, lane, C, m);
         if (has_in) await_granules<C>(kp, in_rsrc, g, k0, lane, m, strip, failed);
-        if (c + 1 < nchunks) {   // next chunk's rows in flight while this chunk computes
-            code_nxt = fetch_codes<C, DNA>(row_rsrc, k0 + C, lane, m);
-            if (has_in) g_nxt = fetch_granules<C>(in_rsrc, k0 + C, lane, m);
-        }
+        if (has_in) g_nxt = fetch_granules<C>(in_rsrc, k0 + C, lane, m);
+        const int code = code_of<DNA>(raw, k0, lane, C, m);
         const bool real = has_in && k0 + lane < m;
         S.feed(lane, C, real ? (int)g.y : -go, real ? (int)g.z : -ge, code);
         S.template run<C>(l63, go, ge, ma, mi);
@@ -393,46 +421,73 @@ __global__ void __launch_bounds__(256) sw_chain_kernel(KParams kp) {
         const bool gout = real && wave == 3 && strip < pd.strips - 1;
         const bool lin = real && wave > 0;
         const bool lout = real && wave < 3 && strip + 1 < pd.strips;
-        const __amdgpu_buffer_rsrc_t in_rsrc = bnd_rsrc(kp, pd, strip - 1);
-        const __amdgpu_buffer_rsrc_t out_rsrc = bnd_rsrc(kp, pd, strip);
+        // granule buffers exist only between groups: boundary g joins group g and g+1
+        const __amdgpu_buffer_rsrc_t in_rsrc = bnd_rsrc(kp, pd, group - 1);
+        const __amdgpu_buffer_rsrc_t out_rsrc = bnd_rsrc(kp, pd, group);
         const __amdgpu_buffer_rsrc_t row_rsrc =
             __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned char*>(kp.seq + pd.row_off), 0, m, RSRC_FLAGS);
         const int nloc = (m + SW - 1 + C - 1) / C;
         const int nT = nloc + 3 * D;
         bool failed = false;
         int c = -wave * D;   // this wave's local chunk
-        int code_nxt = fetch_codes<C, DNA>(row_rsrc, c * C, lane, m);
-        u32x4 g_nxt = gin ? fetch_granules<C>(in_rsrc, c * C, lane, m) : u32x4{0u, 0u, 0u, 0u};
-        for (int T = 0; T < nT; ++T, ++c) {
-            const int k0 = c * C;
-            const bool active = c >= 0 && c < nloc;
-            const int code = code_nxt;
-            u32x4 g = g_nxt;
-            if (gin && active) await_granules<C>(kp, in_rsrc, g, k0, lane, m, strip, failed);
-            code_nxt = fetch_codes<C, DNA>(row_rsrc, k0 + C, lane, m);
-            if (gin) g_nxt = fetch_granules<C>(in_rsrc, k0 + C, lane, m);
-            int hg_in = -go, eh_in = -ge;
-            const int row = k0 + lane;
-            if (active && row >= 0 && row < m && lane < C) {
-                if (gin) {
-                    hg_in = (int)g.y; eh_in = (int)g.z;
-                } else if (lin) {
-                    const int2 v = ring[wave - 1][row & (R - 1)];
-                    hg_in = v.x; eh_in = v.y;
-                }
+        // Row bytes and (wave 0) granules are prefetched TWO chunks ahead into two
+        // buffers that the 2x-unrolled loop refills in place (no register
+        // rotation, hence no wait at the back-edge).  A one-chunk lead is shorter
+        // than the sc1 store->load round trip: a consumer that has caught up
+        // would miss and re-poll on every chunk; with two, one initial miss sets
+        // a lag after which every prefetch hits.  The loop is instantiated per
+        // granule role so that its global loads/stores are unconditional (rows
+        // outside the chunk's range are predicated by the OOR offset) and the
+        // compiler can count vmcnt exactly instead of draining at every join.
+        auto chunk_loop = [&](auto gin_c, auto gout_c) __attribute__((always_inline)) {
+            constexpr bool GIN = decltype(gin_c)::value, GOUT = decltype(gout_c)::value;
+            unsigned r0 = fetch_raw(row_rsrc, c * C, lane, C, m), r1 = fetch_raw(row_rsrc, c * C + C, lane, C, m);
+            u32x4 g0 = u32x4{0u, 0u, 0u, 0u}, g1 = g0;
+            if constexpr (GIN) {
+                g0 = fetch_granules<C>(in_rsrc, c * C, lane, m);
+                g1 = fetch_granules<C>(in_rsrc, c * C + C, lane, m);
             }
-            S.feed(lane, C, hg_in, eh_in, code);
-            S.template run<C>(l63, go, ge, ma, mi);
-            if (active) {
-                if (gout) {
+            auto chunk = [&](const int cc, u32x4& gbuf, unsigned& rbuf) __attribute__((always_inline)) {
+                const int k0 = cc * C;
+                const bool active = cc >= 0 && cc < nloc;
+                // consume the buffers before refilling them, so each refill can
+                // land in the registers the loop carries (no back-edge copies)
+                if constexpr (GIN) await_granules<C>(kp, in_rsrc, gbuf, k0, lane, m, strip, failed);
+                const int code = code_of<DNA>(rbuf, k0, lane, C, m);
+                int hg_in = -go, eh_in = -ge;
+                const int row = k0 + lane;
+                if (active && row >= 0 && row < m && lane < C) {
+                    if constexpr (GIN) {
+                        hg_in = (int)gbuf.y; eh_in = (int)gbuf.z;
+                    } else if (lin) {
+                        const int2 v = ring[wave - 1][row & (R - 1)];
+                        hg_in = v.x; eh_in = v.y;
+                    }
+                }
+                rbuf = fetch_raw(row_rsrc, k0 + 2 * C, lane, C, m);
+                if constexpr (GIN) gbuf = fetch_granules<C>(in_rsrc, k0 + 2 * C, lane, m);
+                S.feed(lane, C, hg_in, eh_in, code);
+                S.template run<C>(l63, go, ge, ma, mi);
+                if constexpr (GOUT) {
                     publish_granules<W, C>(kp, out_rsrc, k0, lane, m, S.IOH, S.IOE);
-                } else if (lout) {
+                } else if (active && lout) {
                     const int row_out = k0 + (lane - (64 - C)) - (SW - 1);
                     if (lane >= 64 - C && row_out >= 0 && row_out < m) ring[wave][row_out & (R - 1)] = make_int2(S.IOH, S.IOE);
                 }
+                __syncthreads();
+            };
+            int T = 0;
+            for (; T + 1 < nT; T += 2, c += 2) {
+                chunk(c, g0, r0);
+                chunk(c + 1, g1, r1);
             }
-            __syncthreads();
-        }
+            if (T < nT) chunk(c, g0, r0);
+        };
+        using T_ = std::true_type;
+        using F_ = std::false_type;
+        if (gin) chunk_loop(T_{}, F_{});
+        else if (gout) chunk_loop(F_{}, T_{});
+        else chunk_loop(F_{}, F_{});
         if (real) S.commit_max(kp, pd, lane);
     }
 }
@@ -569,16 +624,12 @@ struct StripDuo {
     }
 };
 
-template <int C>
-__device__ __forceinline__ unsigned fetch_codes_duo(const __amdgpu_buffer_rsrc_t r0, const __amdgpu_buffer_rsrc_t r1,
-                                                    int k0, int lane, const DuoDesc& d) {
+__device__ __forceinline__ unsigned codes_duo(unsigned raw0, unsigned raw1, int k0, int lane, int C, const DuoDesc& d) {
     const int row = k0 + lane;
     const bool l0 = lane < C && row >= 0 && row < d.m[0];
     const bool l1 = lane < C && row >= 0 && row < d.m[1];
-    const unsigned c0 = __builtin_amdgcn_raw_buffer_load_b8(r0, l0 ? (unsigned)row : OOR, 0, 0);
-    const unsigned c1 = __builtin_amdgcn_raw_buffer_load_b8(r1, l1 ? (unsigned)row : OOR, 0, 0);
-    const unsigned s0 = l0 ? (unsigned)dna_code(c0) : 13u;
-    const unsigned s1 = l1 ? (unsigned)dna_code(c1) + 4u : 13u;
+    const unsigned s0 = l0 ? (unsigned)dna_code(raw0) : 13u;
+    const unsigned s1 = l1 ? (unsigned)dna_code(raw1) + 4u : 13u;
     return 0x0C000C00u | (s1 << 16) | s0;
 }
 
@@ -603,17 +654,17 @@ __device__ void strip_pass_duo(const KParams& kp, const DuoDesc& d, const int st
         __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned char*>(kp.seq + d.row_off[1]), 0, d.m[1], RSRC_FLAGS);
     const int nchunks = (m + SW - 1 + C - 1) / C;
     bool failed = false;
-    unsigned code_nxt = fetch_codes_duo<C>(r0, r1, 0, lane, d);
+    unsigned raw0_nxt = fetch_raw(r0, 0, lane, C, d.m[0]), raw1_nxt = fetch_raw(r1, 0, lane, C, d.m[1]);
     u32x4 g_nxt = has_in ? fetch_granules<C>(in_rsrc, 0, lane, m) : u32x4{0u, 0u, 0u, 0u};
     for (int c = 0; c < nchunks; ++c) {
         const int k0 = c * C;
-        const unsigned code = code_nxt;
+        const unsigned raw0 = raw0_nxt, raw1 = raw1_nxt;
         u32x4 g = g_nxt;
+        raw0_nxt = fetch_raw(r0, k0 + C, lane, C, d.m[0]);
+        raw1_nxt = fetch_raw(r1, k0 + C, lane, C, d.m[1]);
         if (has_in) await_granules<C>(kp, in_rsrc, g, k0, lane, m, strip, failed);
-        if (c + 1 < nchunks) {
-            code_nxt = fetch_codes_duo<C>(r0, r1, k0 + C, lane, d);
-            if (has_in) g_nxt = fetch_granules<C>(in_rsrc, k0 + C, lane, m);
-        }
+        if (has_in) g_nxt = fetch_granules<C>(in_rsrc, k0 + C, lane, m);
+        const unsigned code = codes_duo(raw0, raw1, k0, lane, C, d);
         if (lane < C) {
             const bool real = has_in && k0 + lane < m;
             S.IOA = real ? g.y : as32(ma2);
