@@ -191,6 +191,17 @@ def main():
     total_cells = cells_rank * world * args.steps
     value = total_cells / t_max / 1e9
 
+    # PCIe-inclusive rate of the synchronous host entry point (H2D of the two
+    # sequences + launch + score D2H): reported beside `value`, never as it
+    host_api = None
+    if rank == 0 and workload == "pair":
+        a_h, b_h = host[:N], host[N:]
+        sw.SmithWatermanScoreCUDA(a_h, b_h)
+        t1 = time.perf_counter()
+        hs = sw.SmithWatermanScoreCUDA(a_h, b_h)
+        host_api = {"gcups": round(N * N / (time.perf_counter() - t1) / 1e9, 3), "score": hs,
+                    "entry": "SmithWatermanScoreCUDA (algoGPU.h:9), host buffers"}
+
     # parity of what was just computed (scores vs the committed golden fixtures)
     parity = "unchecked"
     gold = load_golden()
@@ -224,13 +235,14 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "int32",
+            "dtype": "u16x2 (packed, exact: scores < 2^16)" if st["mode"] == 3 else "int32",
             "data": "synthetic (uniform ACGT, mt19937_64 seeds as cudaSmithM.cu:200-212), resident in HBM",
             "config": dict(cfg, params=list(params), W=st["W"], C=st["C"], kernel_items=st["items"],
                            blocks=st["blocks"]),
             "kernel_ms_per_launch": round(avg_kern_ms, 4),
             "kernel_gcups": round(per_launch_cells / (avg_kern_ms * 1e-3) / 1e9, 3),
             "parity": parity,
+            "host_api": host_api,
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "note": "achieved = n*m*12 B (int32 H,E,F per cell, SURVEY 8d) / avg kernel time; "

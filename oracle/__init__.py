@@ -49,6 +49,9 @@ def build() -> None:
     subprocess.run(["make", "-s", "-C", HERE, "all"], check=True)
     if os.path.isdir("/root/reference"):
         subprocess.run(["make", "-s", "-C", HERE, "ref"], check=True)
+        # the reference harness linked against the MI355X library (needs it built)
+        if os.path.exists(os.path.join(HERE, "..", "concurrentproject_amd", "libswmi355.so")):
+            subprocess.run(["make", "-s", "-C", HERE, "harness"], check=True)
 
 
 def lib():

@@ -111,6 +111,24 @@ def test_config_c3_batch_1024(engine, golden):
     assert engine.score_batch(pairs) == c["scores"]
 
 
+def test_config_c4_batch_8192_device(engine, golden):
+    """C4: 8192 pairs of N=8192 (seeds 8192+k) scored from one HBM arena through
+    the device entry point; every score against the committed CPU golden."""
+    import torch
+    c = golden("configs.json")["C4"]
+    N, P = c["N"], c["npairs"]
+    arena = torch.from_numpy(engine.gen_batch(c["seed_base"], P, N)).cuda()
+    scores = torch.full((P,), -1, dtype=torch.int32, device="cuda")
+    offs_a = [2 * N * k for k in range(P)]
+    offs_b = [2 * N * k + N for k in range(P)]
+    s = torch.cuda.current_stream()
+    engine.score_batch_device(arena.data_ptr(), offs_a, [N] * P, offs_b, [N] * P, scores.data_ptr(),
+                              flags=1, stream=s.cuda_stream)
+    torch.cuda.synchronize()
+    engine.stream_status(s.cuda_stream)
+    assert scores.cpu().tolist() == c["scores"]
+
+
 def test_every_variant_ragged(engine, oracle_mod):
     """Each (W, C) kernel variant, DNA and raw-byte paths, on ragged shapes around
     the strip widths 64*W and chunk sizes, in one batch and one at a time."""
