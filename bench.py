@@ -238,7 +238,8 @@ def main():
             "dtype": "u16x2 (packed, exact: scores < 2^16)" if st["mode"] == 3 else "int32",
             "data": "synthetic (uniform ACGT, mt19937_64 seeds as cudaSmithM.cu:200-212), resident in HBM",
             "config": dict(cfg, params=list(params), W=st["W"], C=st["C"], kernel_items=st["items"],
-                           blocks=st["blocks"]),
+                           blocks=st["blocks"], kernel={0: "strip", 1: "pairwg", 2: "chain", 3: "duo",
+                                                        4: "flow"}.get(st["mode"], st["mode"])),
             "kernel_ms_per_launch": round(avg_kern_ms, 4),
             "kernel_gcups": round(per_launch_cells / (avg_kern_ms * 1e-3) / 1e9, 3),
             "parity": parity,

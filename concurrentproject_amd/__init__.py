@@ -26,7 +26,8 @@ __all__ = [
 ]
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libswmi355.so")
+# SWMI355_LIB selects an instrumented build (tools/trace_flow.py); default: the in-tree library
+LIB_PATH = os.environ.get("SWMI355_LIB") or os.path.join(HERE, "libswmi355.so")
 SW_FLAG_DNA, SW_FLAG_BYTES = 1, 2
 
 

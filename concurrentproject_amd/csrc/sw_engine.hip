@@ -56,7 +56,7 @@ std::mutex g_param_mu;
 Params g_params;
 
 std::atomic<long long> g_opt_W{0}, g_opt_C{0}, g_opt_bytes{0}, g_opt_timeout{30}, g_opt_blocks{0}, g_opt_orient{0},
-    g_opt_mode{-1};
+    g_opt_mode{-1}, g_opt_trace{0};
 
 // orientation: 0 = engine policy, 1 = seq1 across lanes (columns), 2 = seq2 across lanes
 bool want_swap(bool single, long long len1, long long len2) {
@@ -248,9 +248,9 @@ void plan(Job& job, int W, int C, bool single) {
         d.bnd_off = g;
         // chain mode hands off through LDS inside a group of 4 strips: granule
         // buffers only between groups; the other modes need one per strip boundary
-        const uint64_t nb = job.mode == MODE_CHAIN ? (uint64_t)((d.strips + 3) / 4 - 1) : (uint64_t)(d.strips - 1);
+        const uint64_t nb = grouped_mode(job.mode) ? (uint64_t)((d.strips + 3) / 4 - 1) : (uint64_t)(d.strips - 1);
         g += nb * (uint64_t)d.m;
-        const int items = job.mode == MODE_CHAIN ? (d.strips + 3) / 4 : job.mode == MODE_STRIP ? d.strips : 1;
+        const int items = grouped_mode(job.mode) ? (d.strips + 3) / 4 : job.mode == MODE_STRIP ? d.strips : 1;
         job.item_base[k + 1] = job.item_base[k] + items;
         cells += (long long)d.n * (long long)d.m;
     }
@@ -303,6 +303,22 @@ void plan_duos(Job& job) {
 // After the alphabet is known: promote an automatic pair-per-workgroup plan to
 // the packed duo kernel when it is exact, or honour a forced duo request.
 int finalize_mode(Job& job, const Params& prm) {
+    // single long DNA pairs: the barrier-free flow kernel when the row codes fit in LDS
+    if (job.mode == MODE_FLOW || (g_opt_mode.load() < 0 && job.mode == MODE_CHAIN)) {
+        int max_m = 0;
+        for (const PairDesc& d : job.pairs) max_m = std::max(max_m, d.m);
+        const bool fits = job.dna && flow_stage_rows(max_m, job.W, job.C) <= flow_stage_max(job.W, job.C);
+        if (fits) {
+            job.mode = MODE_FLOW;
+        } else if (job.mode == MODE_FLOW) {
+            if (g_opt_mode.load() == MODE_FLOW) {
+                set_err("flow mode needs {A,C,G,T} rows that fit in LDS (m <= %d at W=%d)",
+                        flow_stage_max(job.W, job.C) - 64 * job.W - 2 * job.C - 80, job.W);
+                return -1;
+            }
+            job.mode = MODE_CHAIN;
+        }
+    }
     const bool forced_duo = job.mode == MODE_DUO;
     if (forced_duo || (g_opt_mode.load() < 0 && job.mode == MODE_PAIRWG)) {
         if (duo_fits(job, prm)) {
@@ -376,7 +392,9 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
     HIPCHK(hipMemsetAsync(c->ctrl.p, 0, sizeof(unsigned), s));   // next_item only; error stays sticky
     HIPCHK(hipMemsetAsync(d_scores, 0, (size_t)nscores * sizeof(int), s));
 
-    LaunchCfg cfg{job.W, job.C, job.dna, 0, job.mode};
+    int max_m = 0;
+    for (const PairDesc& d : job.pairs) max_m = std::max(max_m, d.m);
+    LaunchCfg cfg{job.W, job.C, job.dna, 0, job.mode, max_m};
     const int wpc = waves_per_cu(c, cfg);
     const int items = job.item_base[np];
     long long blocks = g_opt_blocks.load();
@@ -384,7 +402,7 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
         const long long cap = (long long)c->cus * std::max(1, wpc / 4);
         // strip mode: 4 independent waves per block; chain: one block per group;
         // pair-per-workgroup: one block per pair (grid-stride over pairs)
-        const long long want = job.mode == MODE_STRIP ? (items + 3) / 4 : job.mode == MODE_CHAIN ? items : (long long)np;   // pairwg/duo: np workgroups
+        const long long want = job.mode == MODE_STRIP ? (items + 3) / 4 : grouped_mode(job.mode) ? items : (long long)np;   // pairwg/duo: np workgroups
         blocks = std::min<long long>(want, cap);
     }
     cfg.blocks = (int)std::max<long long>(1, blocks);
@@ -412,6 +430,7 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
         kp.pen[q] = w;
     }
     kp.timeout_ticks = g_opt_timeout.load() * 100000000LL;   // s_memrealtime: 100 MHz
+    kp.trace = reinterpret_cast<unsigned long long*>(g_opt_trace.load());
 
     if (time_kernel) HIPCHK(hipEventRecord(c->ev0, s));
     HIPCHK(launch_sw_strip(cfg, kp, s));
@@ -727,11 +746,13 @@ int sw_set_option(const char* key, long long v) {
     } else if (k == "blocks") {
         if (v < 0) return -1;
         g_opt_blocks = v;
+    } else if (k == "trace") {   // device buffer of 4 u64 per strip (tools only), 0 = off
+        g_opt_trace = v;
     } else if (k == "orient") {
         if (v < 0 || v > 2) return -1;
         g_opt_orient = v;
     } else if (k == "mode") {
-        if (v < -1 || v > 3) return -1;
+        if (v < -1 || v > 4) return -1;
         g_opt_mode = v;
     } else {
         set_err("unknown option '%s'", key);
@@ -749,6 +770,7 @@ long long sw_get_option(const char* key) {
     if (k == "timeout") return g_opt_timeout;
     if (k == "blocks") return g_opt_blocks;
     if (k == "orient") return g_opt_orient;
+    if (k == "trace") return g_opt_trace;
     if (k == "mode") return g_opt_mode;
     return -1;
 }

@@ -53,8 +53,13 @@ struct alignas(16) Granule {
     unsigned int chk;
 };
 
+// Torn-read guard of a 16-B granule {tag, hg, eh, chk}: injective in each of
+// tag, hg and eh for fixed others, so a granule mixing dwords of two writes
+// (different epoch, or a stale value) fails the check.  Multiply-free: XORs
+// and one rotate (v_xor3 / v_alignbit), on the consumer's critical path.
 __host__ __device__ inline unsigned granule_chk(unsigned tag, int hg, int eh, int row) {
-    return tag ^ (unsigned)hg * 0x85EBCA6Bu ^ (unsigned)eh * 0xC2B2AE35u ^ (unsigned)row * 0x9E3779B9u ^ 0x5BD1E995u;
+    const unsigned e = (unsigned)eh;
+    return tag ^ (unsigned)hg ^ ((e << 13) | (e >> 19)) ^ ((unsigned)row << 7) ^ 0x5BD1E995u;
 }
 
 struct KParams {
@@ -72,6 +77,7 @@ struct KParams {
     unsigned pen[4];              // duo mode: per column code, 4 penalty bytes MATCH - s (row code 0..3)
     const DuoDesc* duos;          // duo mode: nduos descriptors (npairs counts duos)
     long long timeout_ticks;      // s_memrealtime ticks (100 MHz) before a spin gives up
+    unsigned long long* trace;    // optional (tools/trace_flow.py): per-strip timestamps, else null
 };
 
 // Grid organisations (sw_kernels.hip):
@@ -79,7 +85,9 @@ struct KParams {
 //   MODE_PAIRWG one workgroup per pair, its 4 waves interleave the strips
 //   MODE_CHAIN  one workgroup per group of 4 consecutive strips, LDS hand-offs
 //   MODE_DUO    one workgroup per two pairs, packed u16 (DNA, small scores)
-enum : int { MODE_STRIP = 0, MODE_PAIRWG = 1, MODE_CHAIN = 2, MODE_DUO = 3 };
+//   MODE_FLOW   as MODE_CHAIN, free-running waves with LDS progress words
+enum : int { MODE_STRIP = 0, MODE_PAIRWG = 1, MODE_CHAIN = 2, MODE_DUO = 3, MODE_FLOW = 4 };
+inline bool grouped_mode(int mode) { return mode == MODE_CHAIN || mode == MODE_FLOW; }
 
 // Host-side launch (sw_kernels.hip).
 struct LaunchCfg {
@@ -88,7 +96,21 @@ struct LaunchCfg {
     bool dna;       // 2-bit ACGT profile path (else raw-byte compare)
     int blocks;     // persistent workgroups (256 threads = 4 waves)
     int mode;       // MODE_*
+    int max_m;      // longest row sequence (MODE_FLOW stages it in LDS)
 };
+
+// MODE_FLOW stages a pair's row codes in LDS: one byte per row plus the
+// prefetch tail; pairs whose rows do not fit use MODE_CHAIN.
+constexpr int LDS_PER_CU = 160 * 1024;
+__host__ __device__ constexpr int flow_stage_rows(int m, int W, int C) { return ((m + 64 * W + 2 * C + 64) + 15) & ~15; }
+__host__ __device__ constexpr int flow_ring_rows(int W, int C) {
+    int r = 256;
+    while (r < 2 * 64 * W + 4 * C) r *= 2;
+    return r;
+}
+// static LDS of sw_flow_kernel<W,C> (rings + sinks + words), rounded up
+__host__ __device__ constexpr int flow_static_lds(int W, int C) { return 3 * flow_ring_rows(W, C) * 8 + 4096; }
+__host__ __device__ constexpr int flow_stage_max(int W, int C) { return LDS_PER_CU - flow_static_lds(W, C); }
 
 hipError_t launch_sw_strip(const LaunchCfg& cfg, const KParams& kp, hipStream_t stream);
 int kernel_waves_per_cu(const LaunchCfg& cfg);     // residency of the chosen variant

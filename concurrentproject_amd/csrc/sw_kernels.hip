@@ -121,7 +121,8 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t bnd_rsrc(const KParams& kp, co
 }
 
 __device__ __forceinline__ bool granule_ok(const u32x4& g, unsigned epoch, int row) {
-    return g.x == epoch && g.w == granule_chk(epoch, (int)g.y, (int)g.z, row);
+    // bitwise, not short-circuit: no exec-mask branch per lane
+    return (g.x == epoch) & (g.w == granule_chk(epoch, (int)g.y, (int)g.z, row));
 }
 
 // ---------------------------------------------------------------------------
@@ -288,7 +289,7 @@ __device__ __forceinline__ void await_granules(const KParams& kp, const __amdgpu
     if (failed) return;
     const int row = k0 + lane;
     const bool need = lane < C && row >= 0 && row < m;
-    const bool ok = !need || granule_ok(g, kp.epoch, row);
+    const bool ok = (!need) | granule_ok(g, kp.epoch, row);
     if (__all(ok)) return;
     const AwaitRes r = await_slow(in_rsrc, g, row, need, kp.epoch, kp.timeout_ticks, kp.ctrl, strip, lane);
     g = r.g;
@@ -489,6 +490,258 @@ __global__ void __launch_bounds__(256) sw_chain_kernel(KParams kp) {
         else if (gout) chunk_loop(F_{}, T_{});
         else chunk_loop(F_{}, F_{});
         if (real) S.commit_max(kp, pd, lane);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Kernel 3b (one long DNA pair, rows staged in LDS, barrier-free): the same
+// groups of 4 consecutive strips as sw_chain_kernel, but the waves free-run
+// and every hand-off inside the workgroup is a progress word in LDS.
+//
+//   * the group's row sequence is converted to 2-bit codes (4 = past the end)
+//     and staged in LDS once per item, while the group still waits for its
+//     left neighbour; no wave touches the row bytes in HBM afterwards;
+//   * wave w publishes its right-edge rows into ring w, then advances prod[w]
+//     (rows published); wave w+1 reads prod[w] and the chunk's ring rows in
+//     one LDS round trip (re-polling both until the word covers the chunk),
+//     then advances cons[w+1] (rows consumed): wave w never overwrites a ring
+//     slot still unread (back-pressure; R >= 2C, so the two waits cannot
+//     deadlock).  DS instructions of one wave execute in issue order, so rows
+//     written before the word are visible to a reader that saw the word; a
+//     compiler barrier keeps the compiler from reordering them;
+//   * the rings start at the border values (H = E = 0), and every slot a
+//     consumer may read past the last row holds either that or a real cell of
+//     the same column, so no per-row range checks are needed (dead rows only
+//     ever see values <= the true maximum);
+//   * lanes that have nothing to publish write to per-lane sink slots, so the
+//     feed / publish code has no exec-mask branches.
+// Lag between strips: 64W + C rows plus one LDS round trip (the lock-step
+// chain pays a barrier per chunk and the slowest wave's chunk every chunk).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int lds_load(const int* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void compiler_fence() { __asm__ __volatile__("" ::: "memory"); }
+
+enum : int { FLOW_NONE = 0, FLOW_GRANULE = 1, FLOW_LDS = 2 };
+#ifndef SW_SPIN_SLEEP
+#define SW_SPIN_SLEEP 1      // s_sleep units (64 cycles) between LDS progress polls
+#endif
+#ifndef SW_GPREF
+#define SW_GPREF 1           // granule prefetch distance of the flow kernel, in chunks (1 measured best)
+#endif
+
+
+// Phase stamps for tools/trace_flow.py: built with -DSW_PHASE_STAMPS
+// (make stamps) to time each chunk's prologue / steps / epilogue in cycles.
+#ifdef SW_PHASE_STAMPS
+__device__ __forceinline__ unsigned long long sw_stamp() {
+    unsigned long long t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+}
+#define SW_STAMP() sw_stamp()
+#else
+#define SW_STAMP() 0ull
+#endif
+
+
+template <int W, int C>
+__global__ void __launch_bounds__(256) sw_flow_kernel(KParams kp) {
+    constexpr int SW = 64 * W;
+    constexpr int R = flow_ring_rows(W, C);
+    static_assert(3 * R * 8 + 4 * 64 * 8 + (4 + 4 + 256 + 1) * 4 <= flow_static_lds(W, C), "flow static LDS");
+    extern __shared__ unsigned char rc[];        // staged row codes (dynamic LDS)
+    __shared__ int2 ring[3][R];
+    __shared__ int2 sink2[4][64];
+    __shared__ int prod[4], cons[4], sink[4][64];
+    __shared__ int s_item;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane((int)(tid >> 6));
+    const bool l63 = lane == 63;
+    const bool lo_lane = lane < C;              // lanes fed at a chunk start
+    const bool hi_lane = lane >= 64 - C;        // lanes holding a chunk's outflow
+    const int go = kp.gap_init, ge = kp.gap_ext, ma = kp.match, mi = kp.mismatch;
+    for (;;) {
+        if (tid == 0) s_item = (int)atomicAdd(&kp.ctrl->next_item, 1u);
+        __syncthreads();   // every wave is done with the previous item
+        const int item = __builtin_amdgcn_readfirstlane(s_item);
+        if (item >= kp.total_items) return;
+        const int pi = find_pair(kp, item);
+        const PairDesc pd = load_pair(kp, pi);
+        const int m = pd.m;
+        const int group = item - kp.item_base[pi];
+        // stage: progress words, border-valued rings, row codes
+        if (tid < 4) { prod[tid] = 0; cons[tid] = 0; }
+        for (int i = tid; i < 3 * R; i += 256) ring[i / R][i % R] = make_int2(-go, -ge);
+        {
+            const __amdgpu_buffer_rsrc_t row_rsrc =
+                __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned char*>(kp.seq + pd.row_off), 0, m, RSRC_FLAGS);
+            const int nst = flow_stage_rows(m, W, C);
+            for (int i = tid * 4; i < nst; i += 1024) {
+                unsigned w = 0;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const unsigned ch = __builtin_amdgcn_raw_buffer_load_b8(row_rsrc, (unsigned)(i + j), 0, 0);
+                    w |= (i + j < m ? (unsigned)dna_code(ch) : 4u) << (8 * j);
+                }
+                *reinterpret_cast<unsigned*>(rc + i) = w;
+            }
+        }
+        __syncthreads();
+        const int strip = 4 * group + wave;
+        if (strip >= pd.strips) continue;
+        Strip<W, true> S;
+        S.setup(kp, pd, strip, lane);
+        const int in_kind = wave > 0 ? FLOW_LDS : strip > 0 ? FLOW_GRANULE : FLOW_NONE;
+        const int out_kind = strip + 1 >= pd.strips ? FLOW_NONE : wave < 3 ? FLOW_LDS : FLOW_GRANULE;
+        const __amdgpu_buffer_rsrc_t in_rsrc = bnd_rsrc(kp, pd, group - 1);
+        const __amdgpu_buffer_rsrc_t out_rsrc = bnd_rsrc(kp, pd, group);
+        const int nloc = (m + SW - 1 + C - 1) / C;
+        bool failed = false;
+        const long long t_start = (long long)__builtin_amdgcn_s_memrealtime();
+        long long t_first = t_start;
+        int spins = 0;
+        unsigned long long cyc_pro = 0, cyc_run = 0, cyc_epi = 0;
+        long long tl[5] = {0, 0, 0, 0, 0};   // SW_TIMELINE: wall clock at chunks 1, 2, 3, 50, 1000
+        // per-lane LDS addresses of the progress words (lane 0) or the sinks
+        int* const prod_out = lane == 0 ? &prod[wave] : &sink[wave][lane];
+        int* const cons_out = lane == 0 ? &cons[wave] : &sink[wave][lane];
+        auto flow_loop = [&](auto in_c, auto out_c) __attribute__((always_inline)) {
+            constexpr int IN = decltype(in_c)::value, OUT = decltype(out_c)::value;
+            u32x4 g0 = u32x4{0u, 0u, 0u, 0u}, g1 = g0;
+            if constexpr (IN == FLOW_GRANULE) {
+                g0 = fetch_granules<C>(in_rsrc, 0, lane, m);
+                if constexpr (SW_GPREF == 2) g1 = fetch_granules<C>(in_rsrc, C, lane, m);
+            }
+            unsigned code_nxt = rc[lane];
+            auto chunk = [&](const int c, u32x4& gbuf) __attribute__((always_inline)) {
+                const int k0 = c * C;
+                const int row = k0 + lane;
+                const unsigned long long ts0 = SW_STAMP();
+#ifdef SW_TIMELINE
+                if (c == 1 || c == 2 || c == 3 || c == 50 || c == 1000) {
+                    const long long now = (long long)__builtin_amdgcn_s_memrealtime();
+                    if (c == 1) tl[0] = now;
+                    else if (c == 2) tl[1] = now;
+                    else if (c == 3) tl[2] = now;
+                    else if (c == 50) tl[3] = now;
+                    else tl[4] = now;
+                }
+#endif
+                int hg_in = -go, eh_in = -ge;
+                int cons_seen = 0;
+                if constexpr (OUT == FLOW_LDS) cons_seen = lds_load(&cons[wave + 1]);   // checked after the steps
+                if constexpr (IN == FLOW_GRANULE) {
+                    await_granules<C>(kp, in_rsrc, gbuf, k0, lane, m, strip, failed);
+                    const bool live = row < m;
+                    hg_in = live ? (int)gbuf.y : -go;
+                    eh_in = live ? (int)gbuf.z : -ge;
+                    if (c == 0) t_first = (long long)__builtin_amdgcn_s_memrealtime();
+                    gbuf = fetch_granules<C>(in_rsrc, k0 + SW_GPREF * C, lane, m);
+                } else if constexpr (IN == FLOW_LDS) {
+                    const int need = min(k0 + C, m);
+                    // the progress word and the rows behind it in one round trip;
+                    // re-read both until the word covers the chunk
+                    int avail = lds_load(&prod[wave - 1]);
+                    compiler_fence();
+                    int2 v = ring[wave - 1][row & (R - 1)];
+                    if (__builtin_amdgcn_readfirstlane(avail) < need) {
+                        do {
+                            __builtin_amdgcn_s_sleep(SW_SPIN_SLEEP);
+                            ++spins;
+                            avail = lds_load(&prod[wave - 1]);
+                            compiler_fence();
+                            v = ring[wave - 1][row & (R - 1)];
+                            if ((long long)__builtin_amdgcn_s_memrealtime() - t_start > kp.timeout_ticks) {
+                                failed = true;   // reported after the strip: no global op in the loop
+                                break;
+                            }
+                        } while (__builtin_amdgcn_readfirstlane(avail) < need);
+                        if (c == 0) t_first = (long long)__builtin_amdgcn_s_memrealtime();
+                    }
+                    hg_in = v.x;
+                    eh_in = v.y;
+                    compiler_fence();
+                    *cons_out = need;   // executes after the ring read (in-order DS)
+                }
+                const int code = (int)code_nxt | 0x0C0C0C00;
+                code_nxt = rc[k0 + C + lane];
+                if (lo_lane) { S.IOH = hg_in; S.IOE = eh_in; S.IOR = code; }
+                const unsigned long long ts1 = SW_STAMP();
+                S.template run<C>(l63, go, ge, ma, mi);
+                const unsigned long long ts2 = SW_STAMP();
+                if constexpr (OUT == FLOW_GRANULE) {
+                    publish_granules<W, C>(kp, out_rsrc, k0, lane, m, S.IOH, S.IOE);
+                } else if constexpr (OUT == FLOW_LDS) {
+                    const int hi = k0 + C - SW;   // last row this chunk completes
+                    if (hi >= 0) {
+                        // ring slots of rows <= hi must have been read: rows < hi + 1 - R consumed
+                        const int floor_rows = hi + 1 - R;
+                        if (__builtin_amdgcn_readfirstlane(cons_seen) < floor_rows) {
+                            do {
+                                __builtin_amdgcn_s_sleep(SW_SPIN_SLEEP);
+                                cons_seen = lds_load(&cons[wave + 1]);
+                                if ((long long)__builtin_amdgcn_s_memrealtime() - t_start > kp.timeout_ticks) {
+                                    failed = true;
+                                    break;
+                                }
+                            } while (__builtin_amdgcn_readfirstlane(cons_seen) < floor_rows);
+                        }
+                        // rows below 0 land in slots of rows not yet written, rows past
+                        // the end in slots already consumed: no range check needed
+                        const int row_out = k0 + (lane - (64 - C)) - (SW - 1);
+                        int2* dst = hi_lane ? &ring[wave][row_out & (R - 1)] : &sink2[wave][lane];
+                        *dst = make_int2(S.IOH, S.IOE);
+                        compiler_fence();
+                        *prod_out = min(hi + 1, m);
+                    }
+                }
+                cyc_pro += ts1 - ts0;
+                cyc_run += ts2 - ts1;
+                cyc_epi += SW_STAMP() - ts2;
+            };
+            int c = 0;
+            for (; c + 1 < nloc; c += 2) {
+                chunk(c, g0);
+                chunk(c + 1, SW_GPREF == 2 ? g1 : g0);
+            }
+            if (c < nloc) chunk(c, g0);
+        };
+        using I0 = std::integral_constant<int, FLOW_NONE>;
+        using I1 = std::integral_constant<int, FLOW_GRANULE>;
+        using I2 = std::integral_constant<int, FLOW_LDS>;
+        if (in_kind == FLOW_LDS) {
+            if (out_kind == FLOW_LDS) flow_loop(I2{}, I2{});
+            else if (out_kind == FLOW_GRANULE) flow_loop(I2{}, I1{});
+            else flow_loop(I2{}, I0{});
+        } else if (in_kind == FLOW_GRANULE) {
+            if (out_kind == FLOW_LDS) flow_loop(I1{}, I2{});
+            else flow_loop(I1{}, I0{});
+        } else {
+            if (out_kind == FLOW_LDS) flow_loop(I0{}, I2{});
+            else flow_loop(I0{}, I0{});
+        }
+        if (kp.trace != nullptr && lane == 0) {
+            unsigned long long* t = kp.trace + 16ull * (unsigned)strip;
+            t[0] = (unsigned long long)t_start;
+            t[1] = (unsigned long long)t_first;
+            t[2] = (unsigned long long)__builtin_amdgcn_s_memrealtime();
+            t[3] = (unsigned long long)spins;
+            t[4] = cyc_pro;
+            t[5] = cyc_run;
+            t[6] = cyc_epi;
+            t[7] = (unsigned long long)nloc;
+            for (int q = 0; q < 5; ++q) t[8 + q] = (unsigned long long)tl[q];
+        }
+        if (failed && lane == 0) {   // an LDS wait gave up (granule waits report themselves too)
+            atomicOr(&kp.ctrl->error, ERR_TIMEOUT);
+            atomicMax(&kp.ctrl->err_item, (unsigned)strip);
+        }
+        S.commit_max(kp, pd, lane);
     }
 }
 
@@ -702,6 +955,21 @@ hipError_t launch_t(const LaunchCfg& cfg, const KParams& kp, hipStream_t s) {
         case MODE_STRIP: hipLaunchKernelGGL((sw_strip_kernel<W, C, DNA>), dim3(cfg.blocks), dim3(256), 0, s, kp); break;
         case MODE_PAIRWG: hipLaunchKernelGGL((sw_pairwg_kernel<W, C, DNA>), dim3(cfg.blocks), dim3(256), 0, s, kp); break;
         case MODE_CHAIN: hipLaunchKernelGGL((sw_chain_kernel<W, C, DNA>), dim3(cfg.blocks), dim3(256), 0, s, kp); break;
+        case MODE_FLOW:
+            if constexpr (DNA) {
+                const int dyn = flow_stage_rows(cfg.max_m, W, C);
+                if (dyn > flow_stage_max(W, C)) return hipErrorInvalidValue;
+                static int dyn_set = 0;   // raise the dynamic-LDS limit once per variant
+                if (dyn > 64 * 1024 && dyn_set == 0) {
+                    const hipError_t e = hipFuncSetAttribute((const void*)sw_flow_kernel<W, C>,
+                                                             hipFuncAttributeMaxDynamicSharedMemorySize, flow_stage_max(W, C));
+                    if (e != hipSuccess) return e;
+                    dyn_set = 1;
+                }
+                hipLaunchKernelGGL((sw_flow_kernel<W, C>), dim3(cfg.blocks), dim3(256), (size_t)dyn, s, kp);
+                break;
+            }
+            return hipErrorInvalidValue;
         case MODE_DUO:
             if constexpr (DNA) { hipLaunchKernelGGL((sw_duo_kernel<W, C>), dim3(cfg.blocks), dim3(256), 0, s, kp); break; }
             return hipErrorInvalidValue;
@@ -716,6 +984,9 @@ int waves_t(int mode) {
         case MODE_STRIP: return occupancy_waves(sw_strip_kernel<W, C, DNA>);
         case MODE_PAIRWG: return occupancy_waves(sw_pairwg_kernel<W, C, DNA>);
         case MODE_CHAIN: return occupancy_waves(sw_chain_kernel<W, C, DNA>);
+        case MODE_FLOW:
+            if constexpr (DNA) return occupancy_waves(sw_flow_kernel<W, C>);
+            return 0;
         case MODE_DUO:
             if constexpr (DNA) return occupancy_waves(sw_duo_kernel<W, C>);
             return 4;

@@ -92,7 +92,8 @@ int sw_stream_status(void* stream);
  *   "orient"   0 = auto, 1 = seq1 spread across lanes, 2 = seq2 across lanes
  *   "mode"     -1 = auto, 0 = independent strip waves, 1 = workgroup per pair,
  *              2 = lock-step strip groups (single long pairs),
- *              3 = packed 16-bit pair duos (DNA batches with scores < 65535)
+ *              3 = packed 16-bit pair duos (DNA batches with scores < 65535),
+ *              4 = free-running strip groups, rows staged in LDS (long DNA pairs)
  * Returns 0, or -1 for an unknown key / bad value. */
 int sw_set_option(const char* key, long long value);
 long long sw_get_option(const char* key);

@@ -95,7 +95,7 @@ def test_config_c2_single_pair_65536(engine, golden):
     # symmetric: the transposed problem gives the same score
     assert engine.SmithWatermanScoreCUDA(b, a) == c["score"]
     # every grid organisation and a wider strip agree at full size
-    for mode in (0, 1, 2):
+    for mode in (0, 1, 2, 4):
         engine.set_option("mode", mode)
         assert engine.SmithWatermanScoreCUDA(a, b) == c["score"], mode
     engine.set_option("mode", -1)
@@ -153,7 +153,7 @@ def test_every_variant_ragged(engine, oracle_mod):
             for force_bytes in (0, 1):
                 engine.set_option("bytes", force_bytes)
                 # independent strips, workgroup per pair, lock-step chain, packed u16 duos (DNA only)
-                for mode in ((0, 1, 2) if force_bytes else (0, 1, 2, 3)):
+                for mode in ((0, 1, 2) if force_bytes else (0, 1, 2, 3, 4)):
                     engine.set_option("mode", mode)
                     assert engine.score_batch(pairs, prm) == exp, (W, C, force_bytes, mode, prm)
                     for (a, b), e in list(zip(pairs, exp))[::4]:

@@ -1,0 +1,88 @@
+#!/usr/bin/env python3
+"""Per-strip timeline of the flow kernel (mode 4) on one long pair.
+
+    python tools/trace_flow.py N C [W]
+
+Each strip records s_memrealtime (100 MHz) at start, when its first inflow
+chunk arrived, and at the end, plus the number of failed progress polls.
+Prints the inter-strip start lag (in-group LDS hops vs cross-group granule
+hops), the run time per strip in ns/step and the poll counts."""
+import json
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    import torch
+    import concurrentproject_amd as sw
+    N = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
+    C = int(sys.argv[2]) if len(sys.argv) > 2 else 32
+    W = int(sys.argv[3]) if len(sys.argv) > 3 else 1
+    torch.cuda.set_device(0)
+    a, b = sw.gen_pair(N, N)
+    arena = torch.from_numpy(np.concatenate([a, b])).cuda()
+    scores = torch.zeros(1, dtype=torch.int32, device="cuda")
+    strips = (N + 64 * W - 1) // (64 * W)
+    trace = torch.zeros(16 * strips, dtype=torch.int64, device="cuda")
+    sw.set_option("mode", 4)
+    sw.set_option("W", W)
+    sw.set_option("C", C)
+    s = torch.cuda.current_stream()
+    for it in range(3):
+        if it == 2:
+            sw.set_option("trace", trace.data_ptr())
+        sw.score_batch_device(arena.data_ptr(), [0], [N], [N], [N], scores.data_ptr(), flags=1, stream=s.cuda_stream)
+        torch.cuda.synchronize()
+    sw.set_option("trace", 0)
+    sw.stream_status(s.cuda_stream)
+    t = trace.cpu().numpy().reshape(strips, 16).astype(np.int64)
+    t0 = t[:, 0].min()
+    start, first, end, spins = (t[:, 0] - t0) * 10, (t[:, 1] - t0) * 10, (t[:, 2] - t0) * 10, t[:, 3]   # ns
+    lag = np.diff(first)
+    ingroup = np.array([(k + 1) % 4 != 0 for k in range(strips - 1)])
+    run_ns = end - first
+    steps = N + 64 * W - 1
+    out = {
+        "N": N, "C": C, "W": W, "score": int(scores.item()), "strips": strips,
+        "total_ms": float(end.max()) / 1e6,
+        "lag_ingroup_ns_median": float(np.median(lag[ingroup])),
+        "lag_crossgroup_ns_median": float(np.median(lag[~ingroup])) if (~ingroup).any() else None,
+        "lag_ingroup_ns_p90": float(np.percentile(lag[ingroup], 90)),
+        "lag_crossgroup_ns_p90": float(np.percentile(lag[~ingroup], 90)) if (~ingroup).any() else None,
+        "sum_lag_ms": float(lag.sum()) / 1e6,
+        "run_ns_per_step_median": float(np.median(run_ns)) / steps,
+        "run_ns_per_step_last": float(run_ns[-1]) / steps,
+        "run_ns_per_step_first": float(run_ns[0]) / steps,
+        "spins_median": float(np.median(spins)), "spins_max": int(spins.max()),
+        "start_spread_ms": float(start.max() - start.min()) / 1e6,
+    }
+    if t[:, 5].any():   # phase stamps (build/libswmi355_stamps.so): cycles per chunk
+        nch = t[:, 7].astype(np.float64)
+        for k, name in ((4, "pro"), (5, "run"), (6, "epi")):
+            out["cyc_per_chunk_" + name] = float(np.median(t[:, k] / nch))
+        out["cyc_per_chunk_strip0"] = [float(t[0, k] / nch[0]) for k in (4, 5, 6)]
+        out["cyc_per_chunk_mid"] = [float(t[5, k] / nch[5]) for k in (4, 5, 6)]
+        out["cyc_per_chunk_last"] = [float(t[-1, k] / nch[-1]) for k in (4, 5, 6)]
+    if t[:, 12].any():   # timeline build: wall clock at chunks 1, 2, 3, 50, 1000
+        tl = (t[:, 8:13] - t0) * 10
+        d50 = np.diff(tl[:, 3]); d1000 = np.diff(tl[:, 4])
+        out["steady_lag_ns_c50_median"] = float(np.median(d50))
+        out["steady_lag_ns_c1000_median"] = float(np.median(d1000))
+        out["steady_lag_ns_c1000_ingroup"] = float(np.median(d1000[ingroup]))
+        out["steady_lag_ns_c1000_crossgroup"] = float(np.median(d1000[~ingroup]))
+        out["chunk_ns_c50_c1000_median"] = float(np.median((tl[:, 4] - tl[:, 3]) / 950.0))
+        out["chunk_ns_c1_c3_median"] = float(np.median((tl[:, 2] - tl[:, 0]) / 2.0))
+        out["first_to_c1_ns_median"] = float(np.median(tl[:, 0] - first))
+        for k in (0, 1, 2, 3, 4, 5, 500, strips - 1):
+            print("TL", k, [int(x) for x in tl[k]], int(first[k]))
+    print(json.dumps(out))
+    for k in list(range(0, 9)) + list(range(strips - 5, strips)):
+        print(k, int(start[k]), int(first[k]), int(end[k]), int(spins[k]), round(run_ns[k] / steps, 2))
+
+
+if __name__ == "__main__":
+    main()
