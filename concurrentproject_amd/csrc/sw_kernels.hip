@@ -618,6 +618,7 @@ __global__ void __launch_bounds__(256) sw_flow_kernel(KParams kp) {
                 if constexpr (SW_GPREF == 2) g1 = fetch_granules<C>(in_rsrc, C, lane, m);
             }
             unsigned code_nxt = rc[lane];
+            int cons_seen = 0;   // OUT == FLOW_LDS: last value read of the consumer's word
             auto chunk = [&](const int c, u32x4& gbuf) __attribute__((always_inline)) {
                 const int k0 = c * C;
                 const int row = k0 + lane;
@@ -633,14 +634,14 @@ __global__ void __launch_bounds__(256) sw_flow_kernel(KParams kp) {
                 }
 #endif
                 int hg_in = -go, eh_in = -ge;
-                int cons_seen = 0;
-                if constexpr (OUT == FLOW_LDS) cons_seen = lds_load(&cons[wave + 1]);   // checked after the steps
                 if constexpr (IN == FLOW_GRANULE) {
                     await_granules<C>(kp, in_rsrc, gbuf, k0, lane, m, strip, failed);
                     const bool live = row < m;
                     hg_in = live ? (int)gbuf.y : -go;
                     eh_in = live ? (int)gbuf.z : -ge;
+#ifdef SW_TIMELINE
                     if (c == 0) t_first = (long long)__builtin_amdgcn_s_memrealtime();
+#endif
                     gbuf = fetch_granules<C>(in_rsrc, k0 + SW_GPREF * C, lane, m);
                 } else if constexpr (IN == FLOW_LDS) {
                     const int need = min(k0 + C, m);
@@ -661,7 +662,9 @@ __global__ void __launch_bounds__(256) sw_flow_kernel(KParams kp) {
                                 break;
                             }
                         } while (__builtin_amdgcn_readfirstlane(avail) < need);
+#ifdef SW_TIMELINE
                         if (c == 0) t_first = (long long)__builtin_amdgcn_s_memrealtime();
+#endif
                     }
                     hg_in = v.x;
                     eh_in = v.y;
@@ -669,8 +672,9 @@ __global__ void __launch_bounds__(256) sw_flow_kernel(KParams kp) {
                     *cons_out = need;   // executes after the ring read (in-order DS)
                 }
                 const int code = (int)code_nxt | 0x0C0C0C00;
-                code_nxt = rc[k0 + C + lane];
                 if (lo_lane) { S.IOH = hg_in; S.IOE = eh_in; S.IOR = code; }
+                compiler_fence();   // keep the next prefetch behind the ring-data wait
+                code_nxt = rc[k0 + C + lane];
                 const unsigned long long ts1 = SW_STAMP();
                 S.template run<C>(l63, go, ge, ma, mi);
                 const unsigned long long ts2 = SW_STAMP();
@@ -681,15 +685,18 @@ __global__ void __launch_bounds__(256) sw_flow_kernel(KParams kp) {
                     if (hi >= 0) {
                         // ring slots of rows <= hi must have been read: rows < hi + 1 - R consumed
                         const int floor_rows = hi + 1 - R;
-                        if (__builtin_amdgcn_readfirstlane(cons_seen) < floor_rows) {
-                            do {
+                        // the consumer's word is re-read only when the cached value no
+                        // longer covers the floor (every ~(R - lag) / C chunks)
+                        if (cons_seen < floor_rows) {
+                            cons_seen = __builtin_amdgcn_readfirstlane(lds_load(&cons[wave + 1]));
+                            while (cons_seen < floor_rows) {
                                 __builtin_amdgcn_s_sleep(SW_SPIN_SLEEP);
-                                cons_seen = lds_load(&cons[wave + 1]);
+                                cons_seen = __builtin_amdgcn_readfirstlane(lds_load(&cons[wave + 1]));
                                 if ((long long)__builtin_amdgcn_s_memrealtime() - t_start > kp.timeout_ticks) {
                                     failed = true;
                                     break;
                                 }
-                            } while (__builtin_amdgcn_readfirstlane(cons_seen) < floor_rows);
+                            }
                         }
                         // rows below 0 land in slots of rows not yet written, rows past
                         // the end in slots already consumed: no range check needed

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Per-strip timeline of the flow kernel (mode 4) on one long pair.
 
-    python tools/trace_flow.py N C [W]
+    python tools/trace_flow.py N C [W] [n_cols]
 
 Each strip records s_memrealtime (100 MHz) at start, when its first inflow
 chunk arrived, and at the end, plus the number of failed progress polls.
@@ -22,11 +22,13 @@ def main():
     N = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
     C = int(sys.argv[2]) if len(sys.argv) > 2 else 32
     W = int(sys.argv[3]) if len(sys.argv) > 3 else 1
+    ncol = int(sys.argv[4]) if len(sys.argv) > 4 else N
     torch.cuda.set_device(0)
     a, b = sw.gen_pair(N, N)
+    a = a[:ncol]
     arena = torch.from_numpy(np.concatenate([a, b])).cuda()
     scores = torch.zeros(1, dtype=torch.int32, device="cuda")
-    strips = (N + 64 * W - 1) // (64 * W)
+    strips = (ncol + 64 * W - 1) // (64 * W)
     trace = torch.zeros(16 * strips, dtype=torch.int64, device="cuda")
     sw.set_option("mode", 4)
     sw.set_option("W", W)
@@ -35,7 +37,8 @@ def main():
     for it in range(3):
         if it == 2:
             sw.set_option("trace", trace.data_ptr())
-        sw.score_batch_device(arena.data_ptr(), [0], [N], [N], [N], scores.data_ptr(), flags=1, stream=s.cuda_stream)
+        sw.set_option("orient", 1)   # a (ncol) across lanes, b (N rows) down
+        sw.score_batch_device(arena.data_ptr(), [0], [ncol], [ncol], [N], scores.data_ptr(), flags=1, stream=s.cuda_stream)
         torch.cuda.synchronize()
     sw.set_option("trace", 0)
     sw.stream_status(s.cuda_stream)
@@ -43,17 +46,17 @@ def main():
     t0 = t[:, 0].min()
     start, first, end, spins = (t[:, 0] - t0) * 10, (t[:, 1] - t0) * 10, (t[:, 2] - t0) * 10, t[:, 3]   # ns
     lag = np.diff(first)
-    ingroup = np.array([(k + 1) % 4 != 0 for k in range(strips - 1)])
+    ingroup = np.array([(k + 1) % 4 != 0 for k in range(strips - 1)], dtype=bool)
     run_ns = end - first
     steps = N + 64 * W - 1
     out = {
-        "N": N, "C": C, "W": W, "score": int(scores.item()), "strips": strips,
+        "N": N, "ncol": ncol, "C": C, "W": W, "score": int(scores.item()), "strips": strips,
         "total_ms": float(end.max()) / 1e6,
-        "lag_ingroup_ns_median": float(np.median(lag[ingroup])),
+        "lag_ingroup_ns_median": float(np.median(lag[ingroup])) if lag.size else None,
         "lag_crossgroup_ns_median": float(np.median(lag[~ingroup])) if (~ingroup).any() else None,
-        "lag_ingroup_ns_p90": float(np.percentile(lag[ingroup], 90)),
+        "lag_ingroup_ns_p90": float(np.percentile(lag[ingroup], 90)) if lag.size else None,
         "lag_crossgroup_ns_p90": float(np.percentile(lag[~ingroup], 90)) if (~ingroup).any() else None,
-        "sum_lag_ms": float(lag.sum()) / 1e6,
+        "sum_lag_ms": float(lag.sum()) / 1e6 if lag.size else 0.0,
         "run_ns_per_step_median": float(np.median(run_ns)) / steps,
         "run_ns_per_step_last": float(run_ns[-1]) / steps,
         "run_ns_per_step_first": float(run_ns[0]) / steps,
@@ -70,14 +73,15 @@ def main():
     if t[:, 12].any():   # timeline build: wall clock at chunks 1, 2, 3, 50, 1000
         tl = (t[:, 8:13] - t0) * 10
         d50 = np.diff(tl[:, 3]); d1000 = np.diff(tl[:, 4])
-        out["steady_lag_ns_c50_median"] = float(np.median(d50))
-        out["steady_lag_ns_c1000_median"] = float(np.median(d1000))
-        out["steady_lag_ns_c1000_ingroup"] = float(np.median(d1000[ingroup]))
-        out["steady_lag_ns_c1000_crossgroup"] = float(np.median(d1000[~ingroup]))
+        med = lambda x: float(np.median(x)) if x.size else None
+        out["steady_lag_ns_c50_median"] = med(d50)
+        out["steady_lag_ns_c1000_median"] = med(d1000)
+        out["steady_lag_ns_c1000_ingroup"] = med(d1000[ingroup])
+        out["steady_lag_ns_c1000_crossgroup"] = med(d1000[~ingroup])
         out["chunk_ns_c50_c1000_median"] = float(np.median((tl[:, 4] - tl[:, 3]) / 950.0))
         out["chunk_ns_c1_c3_median"] = float(np.median((tl[:, 2] - tl[:, 0]) / 2.0))
         out["first_to_c1_ns_median"] = float(np.median(tl[:, 0] - first))
-        for k in (0, 1, 2, 3, 4, 5, 500, strips - 1):
+        for k in sorted({k for k in (0, 1, 2, 3, 4, 5, 500, strips - 1) if k < strips}):
             print("TL", k, [int(x) for x in tl[k]], int(first[k]))
     print(json.dumps(out))
     for k in list(range(0, 9)) + list(range(strips - 5, strips)):
