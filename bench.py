@@ -239,7 +239,7 @@ def main():
             "data": "synthetic (uniform ACGT, mt19937_64 seeds as cudaSmithM.cu:200-212), resident in HBM",
             "config": dict(cfg, params=list(params), W=st["W"], C=st["C"], kernel_items=st["items"],
                            blocks=st["blocks"], kernel={0: "strip", 1: "pairwg", 2: "chain", 3: "duo",
-                                                        4: "flow"}.get(st["mode"], st["mode"])),
+                                                        4: "flow", 5: "flow2"}.get(st["mode"], st["mode"])),
             "kernel_ms_per_launch": round(avg_kern_ms, 4),
             "kernel_gcups": round(per_launch_cells / (avg_kern_ms * 1e-3) / 1e9, 3),
             "parity": parity,

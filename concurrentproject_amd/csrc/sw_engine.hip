@@ -302,11 +302,43 @@ void plan_duos(Job& job) {
 
 // After the alphabet is known: promote an automatic pair-per-workgroup plan to
 // the packed duo kernel when it is exact, or honour a forced duo request.
+// MODE_FLOW2 (sw_flow2.hip): W = 1, DNA, every score byte s + G_INIT a signed
+// byte above the -128 sentinel, and the row codes fit in LDS.
+bool flow2_fits(const Job& job, const Params& p, int max_m) {
+    return job.dna && job.W == 1 && flow2_variant_exists(job.C) && p.match + p.gap_init <= 127 &&
+           p.mismatch + p.gap_init >= -127 && flow2_stage_bytes(max_m, job.C) <= flow2_stage_max(job.C);
+}
+
+// Re-plan a grouped job for MODE_FLOW2: strips of 64 columns overlapping by one.
+void plan_flow2(Job& job) {
+    job.mode = MODE_FLOW2;
+    uint64_t g = 0;
+    for (size_t k = 0; k < job.pairs.size(); ++k) {
+        PairDesc& d = job.pairs[k];
+        d.strips = flow2_strips(d.n);
+        d.bnd_off = g;
+        g += (uint64_t)((d.strips + 3) / 4 - 1) * (uint64_t)d.m;
+        job.item_base[k + 1] = job.item_base[k] + (d.strips + 3) / 4;
+    }
+    job.bnd_granules = g;
+}
+
 int finalize_mode(Job& job, const Params& prm) {
+    int max_m = 0;
+    for (const PairDesc& d : job.pairs) max_m = std::max(max_m, d.m);
+    if (job.mode == MODE_FLOW2 || (g_opt_mode.load() < 0 && job.mode == MODE_CHAIN)) {
+        if (flow2_fits(job, prm, max_m)) {
+            plan_flow2(job);
+            return 0;
+        }
+        if (job.mode == MODE_FLOW2) {
+            set_err("flow2 mode needs W=1, C in {16,32,64}, {A,C,G,T} rows that fit in LDS and "
+                    "-127 <= MISMATCH+G_INIT, MATCH+G_INIT <= 127");
+            return -1;
+        }
+    }
     // single long DNA pairs: the barrier-free flow kernel when the row codes fit in LDS
     if (job.mode == MODE_FLOW || (g_opt_mode.load() < 0 && job.mode == MODE_CHAIN)) {
-        int max_m = 0;
-        for (const PairDesc& d : job.pairs) max_m = std::max(max_m, d.m);
         const bool fits = job.dna && flow_stage_rows(max_m, job.W, job.C) <= flow_stage_max(job.W, job.C);
         if (fits) {
             job.mode = MODE_FLOW;
@@ -349,7 +381,7 @@ int waves_per_cu(Ctx* c, const LaunchCfg& cfg) {
     const int key = cfg.mode * 100000 + cfg.W * 1000 + cfg.C * 2 + (cfg.dna ? 1 : 0);
     auto it = c->waves_cache.find(key);
     if (it != c->waves_cache.end()) return it->second;
-    int w = kernel_waves_per_cu(cfg);
+    int w = cfg.mode == MODE_FLOW2 ? flow2_waves_per_cu(cfg.C) : kernel_waves_per_cu(cfg);
     if (w <= 0) w = 4;
     c->waves_cache[key] = w;
     return w;
@@ -358,7 +390,7 @@ int waves_per_cu(Ctx* c, const LaunchCfg& cfg) {
 // Enqueue the launch for a planned job whose sequences are in `d_seq`.
 int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int* d_scores, int nscores,
             hipStream_t s, bool time_kernel) {
-    if (!variant_exists(job.W, job.C)) {
+    if (job.mode == MODE_FLOW2 ? !flow2_variant_exists(job.C) : !variant_exists(job.W, job.C)) {
         set_err("no kernel variant for W=%d C=%d", job.W, job.C);
         return -1;
     }
@@ -424,6 +456,11 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
     kp.gap_init = prm.gap_init;
     kp.gap_ext = prm.gap_ext;
     profile_words(prm, kp.prof);
+    for (int q = 0; q < 4; ++q) {   // flow2: signed bytes s(q, r) + G_INIT
+        unsigned w = 0;
+        for (int r = 0; r < 4; ++r) w |= (unsigned)(((r == q ? prm.match : prm.mismatch) + prm.gap_init) & 0xFF) << (8 * r);
+        kp.prof2[q] = w;
+    }
     for (int q = 0; q < 4; ++q) {   // duo: penalty bytes MATCH - s(r, q)
         unsigned w = 0;
         for (int r = 0; r < 4; ++r) w |= (unsigned)(r == q ? 0 : prm.match - prm.mismatch) << (8 * r);
@@ -433,7 +470,7 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
     kp.trace = reinterpret_cast<unsigned long long*>(g_opt_trace.load());
 
     if (time_kernel) HIPCHK(hipEventRecord(c->ev0, s));
-    HIPCHK(launch_sw_strip(cfg, kp, s));
+    HIPCHK(job.mode == MODE_FLOW2 ? launch_sw_flow2(cfg, kp, s) : launch_sw_strip(cfg, kp, s));
     if (time_kernel) HIPCHK(hipEventRecord(c->ev1, s));
 
     t_stats = sw_stats{};
@@ -752,7 +789,7 @@ int sw_set_option(const char* key, long long v) {
         if (v < 0 || v > 2) return -1;
         g_opt_orient = v;
     } else if (k == "mode") {
-        if (v < -1 || v > 4) return -1;
+        if (v < -1 || v > 5) return -1;
         g_opt_mode = v;
     } else {
         set_err("unknown option '%s'", key);

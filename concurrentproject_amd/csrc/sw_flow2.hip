@@ -1,0 +1,360 @@
+// sw_flow2.hip -- the single-long-pair kernel (BASELINE config 2: one DNA pair,
+// N = 65536) for gfx950.  Same recurrence and clamped arithmetic as
+// sw_kernels.hip (main.cpp:54-66, DESIGN.md "Arithmetic"); what changes is how
+// few instructions one anti-diagonal step costs.  For one long pair the time is
+// (m + strips x lag) steps of ONE wave per SIMD issuing alone (~4 cycles per
+// instruction, 2-4x more for LDS stores: MI355X_MICROARCH.md, LDS), so every
+// instruction of the step is on the critical path.
+//
+// Layout: a wave owns a strip of 64 columns, lane l = column 63*s + l.  Strips
+// OVERLAP by one column: lane 0 of strip s+1 recomputes column 63*(s+1), the
+// column of lane 63 of strip s.  Its left inputs (H - G_INIT, E - G_EXT of
+// column 63s+62) are then exactly the values lane 63 of strip s computes in its
+// own DPP step, so the hand-off needs no extra arithmetic.
+//
+// One step (lane l, row i = k - l), 10.5 VALU for 64 cells:
+//   t    = L0 + s               L0 = last step's hgL (the diagonal); s is a
+//                               signed byte s(q,d) + G_INIT, taken with an SDWA
+//                               byte select from a v_perm_b32 of 4 rows' codes
+//   IOx' = wave_shl1(IOx), lane 63 <- last step's (hgL, ehL)
+//                               rotating I/O registers: lanes [0, C) enter a
+//                               chunk holding the inflow rows, lanes [64-C, 64)
+//                               leave it holding the outflow rows (one LDS read
+//                               and one LDS write per chunk, not per step)
+//   hgL  = v_add_u32_dpp(old = IOH, H, -G_INIT)   lanes 1..63: H[l-1] - G_INIT,
+//   ehL  = v_add_u32_dpp(old = IOE, E, -G_EXT)    lane 0 keeps the inflow row
+//   E    = max3(ehL, hgL, 0)    clamped E (H never sees E < 0)
+//   F    = max3(fh, hgO, 0),  fh = F - G_EXT,  hgO = H - G_INIT
+//   H    = max3(t, E, F),  M = max(M, t)
+//
+// Hand-offs: wave w -> w+1 of a workgroup through an LDS ring with progress
+// words (as sw_flow_kernel); the workgroup edges through tagged HBM granules
+// (sw_device.h).  Work items (groups of 4 strips) are claimed in order, so a
+// producer is always resident: no co-residency assumption, any grid size.
+// Every spin is bounded by s_memrealtime and reports ERR_TIMEOUT.
+#include <type_traits>
+
+#include "sw_device.h"
+
+namespace swmi {
+namespace {
+
+constexpr int F2_R = 256;   // ring rows per link (power of two, >= 2C + 64)
+#ifndef SW_F2_SPEC
+#define SW_F2_SPEC 2        // the next chunk's inflow is read after SW_F2_SPEC/4 of a chunk's steps
+#endif
+
+constexpr int DPP_WAVE_SHL1 = 0x130;
+
+// v_add_u32_dpp wave_shr:1 with the destination tied to 'old': lanes 1..63 get
+// src[l-1] + k, lane 0 (no source, bound_ctrl off) keeps old.  Inline asm because
+// no builtin ties a DPP-VOP2 destination to a live register.  The hazard a VALU
+// write of src -> DPP read of src needs (2 wait states) is invisible to the
+// compiler inside asm, so the asm takes 'after', a value computed from src
+// through >= 2 dependent instructions: the asm cannot issue sooner.
+__device__ __forceinline__ int dpp_add_shr1_tied(int old, int src, int k, int after) {
+    asm("v_add_u32_dpp %0, %1, %2 wave_shr:1 row_mask:0xf bank_mask:0xf ; dep %3"
+        : "+v"(old) : "v"(src), "v"(k), "v"(after));
+    return old;
+}
+
+// gfx950 LDS serves unaligned dword reads (ds_read_b32 at any byte address)
+__device__ __forceinline__ unsigned load_u32_unaligned(const unsigned char* p) {
+    unsigned v;
+    __builtin_memcpy(&v, p, 4);
+    return v;
+}
+
+// signed byte b of w (SDWA src_sel:BYTE_b with sext)
+template <int B>
+__device__ __forceinline__ int sbyte(unsigned w) {
+    if constexpr (B == 3) return (int)w >> 24;
+    else return (int)(signed char)(w >> (8 * B));
+}
+
+template <int C>
+__global__ void __launch_bounds__(256) sw_flow2_kernel(KParams kp) {
+    static_assert(C % 4 == 0 && 64 % C == 0 && 2 * C + 64 <= F2_R, "chunk");
+    constexpr int R = F2_R;
+    extern __shared__ unsigned char rc[];    // rc[row + 64]: 4..7 = A,C,G,T; 0 = no row
+    __shared__ int2 ring[4][R];              // ring w: outflow rows of wave w (row r in slot r mod R)
+    __shared__ int2 sink[4][64];             // lanes that publish nothing write here
+    __shared__ int prod[4], cons[4], psink[4][64];
+    __shared__ int s_item;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane((int)(tid >> 6));
+    const int go = kp.gap_init, ge = kp.gap_ext;
+    for (;;) {
+        if (tid == 0) s_item = (int)atomicAdd(&kp.ctrl->next_item, 1u);
+        __syncthreads();   // every wave is done with the previous item
+        const int item = __builtin_amdgcn_readfirstlane(s_item);
+        if (item >= kp.total_items) return;
+        const int pi = find_pair(kp, item);
+        const PairDesc pd = load_pair(kp, pi);
+        const int m = pd.m;
+        const int group = item - kp.item_base[pi];
+        const int nloc = (m + 64 + C - 1) / C;   // lane 63's last row is out at step m + 63
+        if (tid < 4) { prod[tid] = 0; cons[tid] = 0; }
+        for (int i = tid; i < 4 * R; i += 256) ring[i / R][i % R] = make_int2(-go, -ge);
+        {
+            const __amdgpu_buffer_rsrc_t row_rsrc =
+                __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned char*>(kp.seq + pd.row_off), 0, m, RSRC_FLAGS);
+            const int nst = flow2_stage_bytes(m, C);
+            for (int i = tid * 4; i < nst; i += 1024) {
+                unsigned w = 0;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int row = i + j - 64;
+                    const bool live = row >= 0 && row < m;
+                    const unsigned ch = __builtin_amdgcn_raw_buffer_load_b8(row_rsrc, live ? (unsigned)row : OOR, 0, 0);
+                    w |= (live ? 4u + (unsigned)dna_code(ch) : 0u) << (8 * j);
+                }
+                *reinterpret_cast<unsigned*>(rc + i) = w;
+            }
+        }
+        __syncthreads();
+        const int strip = 4 * group + wave;
+        if (strip >= pd.strips) continue;
+        const int col = 63 * strip + lane;
+        const unsigned prof = col < pd.n ? kp.prof2[dna_code(kp.seq[pd.col_off + col])] : 0x80808080u;
+        const int in_kind = wave > 0 ? FLOW_LDS : strip > 0 ? FLOW_GRANULE : FLOW_NONE;
+        const int out_kind = strip + 1 >= pd.strips ? FLOW_NONE : wave < 3 ? FLOW_LDS : FLOW_GRANULE;
+        const __amdgpu_buffer_rsrc_t in_rsrc = bnd_rsrc(kp, pd, group - 1);
+        const __amdgpu_buffer_rsrc_t out_rsrc = bnd_rsrc(kp, pd, group);
+        const long long t_start = (long long)__builtin_amdgcn_s_memrealtime();
+        bool failed = false;
+        long long t_first = t_start;
+        long long tl[5] = {0, 0, 0, 0, 0};   // SW_TIMELINE: wall clock at chunks 1, 2, 3, 50, 1000
+        int H = 0, E = 0, fh = -ge, hgO = -go, L0 = -go, ehP = -ge, M = 0;
+        int IOH = -go, IOE = -ge;                 // rotating I/O registers (see the step)
+        // -G_INIT, -G_EXT kept in VGPRs (operands of the DPP-adds, which take no SGPR)
+        int neggo, negge;
+        asm volatile("v_mov_b32 %0, %1" : "=v"(neggo) : "s"(-go));
+        asm volatile("v_mov_b32 %0, %1" : "=v"(negge) : "s"(-ge));
+        // progress words are written by every lane: lane 0 to the word, the others to sinks
+        // (no exec-mask branch, so the compiler counts LDS operations exactly)
+        int* const prod_out = lane == 0 ? &prod[wave] : &psink[wave][lane];
+        int* const cons_out = lane == 0 ? &cons[wave] : &psink[wave][lane];
+        int2* const in_ring = ring[wave > 0 ? wave - 1 : 0];
+        int2* const out_ring = ring[wave];
+        // per-lane code address: lane l reads rows k - l .. k - l + 3 (unaligned dword)
+        const unsigned char* const code_base = rc + 64 - lane;
+
+        auto flow_loop = [&](auto in_c, auto out_c) __attribute__((always_inline)) {
+            constexpr int IN = decltype(in_c)::value, OUT = decltype(out_c)::value;
+            u32x4 gpre = u32x4{0u, 0u, 0u, 0u};
+            if constexpr (IN == FLOW_GRANULE) gpre = fetch_granules<C>(in_rsrc, 0, lane, m);
+            unsigned D[C / 4];
+#pragma unroll
+            for (int u = 0; u < C / 4; ++u) D[u] = load_u32_unaligned(code_base + 4 * u);
+            int cons_seen = 0;
+            int spec_avail = -1;                 // progress word read with spec_v (-1: none)
+            int2 spec_v = make_int2(0, 0);
+            // ---- publish the last chunk's outflow: lane L >= 64 - C holds row k0 - 128 + L
+            auto publish = [&](const int k0) __attribute__((always_inline)) {
+                const int row_out = k0 - 128 + lane;
+                if constexpr (OUT == FLOW_LDS) {
+                    // ring slots of rows < k0 - 64 - R must have been read
+                    const int floor_rows = k0 - 64 - R;
+                    if (cons_seen < floor_rows) {
+                        cons_seen = __builtin_amdgcn_readfirstlane(lds_load(&cons[wave + 1]));
+                        while (cons_seen < floor_rows) {
+                            __builtin_amdgcn_s_sleep(SW_SPIN_SLEEP);
+                            cons_seen = __builtin_amdgcn_readfirstlane(lds_load(&cons[wave + 1]));
+                            if ((long long)__builtin_amdgcn_s_memrealtime() - t_start > kp.timeout_ticks) {
+                                failed = true;
+                                break;
+                            }
+                        }
+                    }
+                    int2* const dst = lane >= 64 - C ? &out_ring[row_out & (R - 1)] : &sink[wave][lane];
+                    *dst = make_int2(IOH, IOE);
+                    compiler_fence();
+                    *prod_out = max(0, k0 - 64);   // after the ring writes (in-order DS)
+                } else if constexpr (OUT == FLOW_GRANULE) {
+                    const bool st = lane >= 64 - C && row_out >= 0 && row_out < m;
+                    u32x4 g;
+                    g.x = kp.epoch;
+                    g.y = (unsigned)IOH;
+                    g.z = (unsigned)IOE;
+                    g.w = granule_chk(kp.epoch, IOH, IOE, row_out);
+                    __builtin_amdgcn_raw_buffer_store_b128(g, out_rsrc, st ? (unsigned)row_out * 16u : OOR, 0, AUX_SC1);
+                }
+            };
+            for (int c = 0; c < nloc; ++c) {
+                const int k0 = c * C;
+#ifdef SW_TIMELINE
+                if (c == 1 || c == 2 || c == 3 || c == 50 || c == 1000) {
+                    const long long now = (long long)__builtin_amdgcn_s_memrealtime();
+                    tl[c == 1 ? 0 : c == 2 ? 1 : c == 3 ? 2 : c == 50 ? 3 : 4] = now;
+                }
+#endif
+                // ---- inflow rows [k0, k0 + C), for lanes [0, C) of the I/O registers
+                int newH, newE;
+                if constexpr (IN == FLOW_GRANULE) {
+                    u32x4 g = gpre;
+                    await_granules<C>(kp, in_rsrc, g, k0, lane, m, strip, failed);
+                    gpre = fetch_granules<C>(in_rsrc, k0 + C, lane, m);
+                    const bool live = k0 + lane < m;
+                    newH = live ? (int)g.y : -go;
+                    newE = live ? (int)g.z : -ge;
+                } else if constexpr (IN == FLOW_LDS) {
+                    // the rows were read speculatively during the last chunk, behind a read
+                    // of the progress word; only if that word did not cover them, poll and re-read
+                    const int need = min(k0 + C, m);
+                    int2 v = spec_v;
+                    if (__builtin_amdgcn_readfirstlane(spec_avail) < need) {
+                        int avail = __builtin_amdgcn_readfirstlane(lds_load(&prod[wave - 1]));
+                        while (avail < need) {
+                            __builtin_amdgcn_s_sleep(SW_SPIN_SLEEP);
+                            avail = __builtin_amdgcn_readfirstlane(lds_load(&prod[wave - 1]));
+                            if ((long long)__builtin_amdgcn_s_memrealtime() - t_start > kp.timeout_ticks) {
+                                failed = true;
+                                break;
+                            }
+                        }
+                        compiler_fence();
+                        v = in_ring[(k0 + (lane & (C - 1))) & (R - 1)];
+                    }
+                    newH = v.x;
+                    newE = v.y;
+                } else {
+                    newH = -go;
+                    newE = -ge;
+                }
+                // ---- scores of the chunk's rows: one v_perm_b32 per 4 rows
+                unsigned P[C / 4];
+#pragma unroll
+                for (int u = 0; u < C / 4; ++u) P[u] = __builtin_amdgcn_perm(prof, 0x80808080u, D[u]);
+                // take the inflow (and the scores) into registers before this chunk's LDS
+                // writes are issued, so the waits for them do not also wait for the writes
+                asm volatile("" : "+v"(newH), "+v"(newE));
+                if (c > 0) publish(k0);
+                IOH = newH;
+                IOE = newE;
+                if constexpr (IN == FLOW_LDS) {
+                    compiler_fence();
+                    *cons_out = k0 + C;   // after the ring read (DS ops execute in order)
+                }
+#ifdef SW_TIMELINE
+                if (c == 0) t_first = (long long)__builtin_amdgcn_s_memrealtime();
+#endif
+#pragma unroll
+                for (int u = 0; u < C / 4; ++u) D[u] = load_u32_unaligned(code_base + k0 + C + 4 * u);
+                // ---- C anti-diagonal steps
+#pragma unroll
+                for (int j = 0; j < C; j += 4) {
+                    if constexpr (IN == FLOW_LDS) {
+                        if (j == SW_F2_SPEC * C / 4) {   // speculative read of the next chunk's inflow
+                            spec_avail = lds_load(&prod[wave - 1]);
+                            compiler_fence();
+                            spec_v = in_ring[(k0 + C + (lane & (C - 1))) & (R - 1)];
+                            compiler_fence();
+                        }
+                    }
+                    auto step = [&](auto b_c) __attribute__((always_inline)) {
+                        constexpr int b = decltype(b_c)::value;
+                        const int t = L0 + sbyte<b>(P[j >> 2]);
+                        // rotate the I/O registers down one lane; lane 63 takes last step's
+                        // (hgL, ehL) = row k - 64 of the next strip's lane 0
+                        const int ioh = __builtin_amdgcn_update_dpp(L0, IOH, DPP_WAVE_SHL1, 0xF, 0xF, false);
+                        const int ioe = __builtin_amdgcn_update_dpp(ehP, IOE, DPP_WAVE_SHL1, 0xF, 0xF, false);
+                        const int F = max3i(fh, hgO, 0);
+                        const int hgL = dpp_add_shr1_tied(IOH, H, neggo, F);     // H -> hgO -> F -> DPP
+                        const int ehL = dpp_add_shr1_tied(IOE, E, negge, hgO);   // E -> H -> hgO -> DPP
+                        IOH = ioh;
+                        IOE = ioe;
+                        E = max3i(ehL, hgL, 0);
+                        fh = F - ge;
+                        H = vmax3(t, E, F);
+                        hgO = H - go;
+                        M = max(M, t);
+                        L0 = hgL;
+                        ehP = ehL;
+                    };
+                    step(std::integral_constant<int, 0>{});
+                    step(std::integral_constant<int, 1>{});
+                    step(std::integral_constant<int, 2>{});
+                    step(std::integral_constant<int, 3>{});
+                }
+            }
+            publish(nloc * C);
+        };
+        using I0 = std::integral_constant<int, FLOW_NONE>;
+        using I1 = std::integral_constant<int, FLOW_GRANULE>;
+        using I2 = std::integral_constant<int, FLOW_LDS>;
+        if (in_kind == FLOW_LDS) {
+            if (out_kind == FLOW_LDS) flow_loop(I2{}, I2{});
+            else if (out_kind == FLOW_GRANULE) flow_loop(I2{}, I1{});
+            else flow_loop(I2{}, I0{});
+        } else if (in_kind == FLOW_GRANULE) {
+            if (out_kind == FLOW_LDS) flow_loop(I1{}, I2{});
+            else flow_loop(I1{}, I0{});
+        } else {
+            if (out_kind == FLOW_LDS) flow_loop(I0{}, I2{});
+            else flow_loop(I0{}, I0{});
+        }
+        if (kp.trace != nullptr && lane == 0) {
+            unsigned long long* t = kp.trace + 16ull * (unsigned)strip;
+            t[0] = (unsigned long long)t_start;
+            t[1] = (unsigned long long)t_first;
+            t[2] = (unsigned long long)__builtin_amdgcn_s_memrealtime();
+            t[7] = (unsigned long long)nloc;
+            for (int q = 0; q < 5; ++q) t[8 + q] = (unsigned long long)tl[q];
+        }
+        if (failed && lane == 0) {
+            atomicOr(&kp.ctrl->error, ERR_TIMEOUT);
+            atomicMax(&kp.ctrl->err_item, (unsigned)strip);
+        }
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) M = max(M, __shfl_xor(M, off));
+        if (lane == 0 && M > 0) atomicMax(&kp.scores[pd.out_idx], M);
+    }
+}
+
+template <int C>
+hipError_t launch_c(const LaunchCfg& cfg, const KParams& kp, hipStream_t s) {
+    const int dyn = flow2_stage_bytes(cfg.max_m, C);
+    if (dyn > flow2_stage_max(C)) return hipErrorInvalidValue;
+    static int dyn_set = 0;   // raise the dynamic-LDS limit once per variant
+    if (dyn > 64 * 1024 && dyn_set == 0) {
+        const hipError_t e = hipFuncSetAttribute((const void*)sw_flow2_kernel<C>,
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, flow2_stage_max(C));
+        if (e != hipSuccess) return e;
+        dyn_set = 1;
+    }
+    hipLaunchKernelGGL((sw_flow2_kernel<C>), dim3(cfg.blocks), dim3(256), (size_t)dyn, s, kp);
+    return hipGetLastError();
+}
+
+template <int C>
+int waves_c() {
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)sw_flow2_kernel<C>, 256, 0) != hipSuccess) return 4;
+    return nb * 4;
+}
+
+}  // namespace
+
+bool flow2_variant_exists(int C) { return C == 16 || C == 32 || C == 64; }
+
+hipError_t launch_sw_flow2(const LaunchCfg& cfg, const KParams& kp, hipStream_t stream) {
+    switch (cfg.C) {
+        case 16: return launch_c<16>(cfg, kp, stream);
+        case 32: return launch_c<32>(cfg, kp, stream);
+        case 64: return launch_c<64>(cfg, kp, stream);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+int flow2_waves_per_cu(int C) {
+    switch (C) {
+        case 16: return waves_c<16>();
+        case 32: return waves_c<32>();
+        case 64: return waves_c<64>();
+        default: return 4;
+    }
+}
+
+}  // namespace swmi

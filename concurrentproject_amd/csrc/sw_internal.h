@@ -74,6 +74,7 @@ struct KParams {
     unsigned epoch;               // != 0, unique per launch
     int match, mismatch, gap_init, gap_ext;
     unsigned prof[4];             // DNA mode: per column code, 4 biased score bytes (row code 0..3)
+    unsigned prof2[4];            // flow2 mode: per column code, 4 signed score bytes s + G_INIT (row code 0..3)
     unsigned pen[4];              // duo mode: per column code, 4 penalty bytes MATCH - s (row code 0..3)
     const DuoDesc* duos;          // duo mode: nduos descriptors (npairs counts duos)
     long long timeout_ticks;      // s_memrealtime ticks (100 MHz) before a spin gives up
@@ -86,8 +87,10 @@ struct KParams {
 //   MODE_CHAIN  one workgroup per group of 4 consecutive strips, LDS hand-offs
 //   MODE_DUO    one workgroup per two pairs, packed u16 (DNA, small scores)
 //   MODE_FLOW   as MODE_CHAIN, free-running waves with LDS progress words
-enum : int { MODE_STRIP = 0, MODE_PAIRWG = 1, MODE_CHAIN = 2, MODE_DUO = 3, MODE_FLOW = 4 };
-inline bool grouped_mode(int mode) { return mode == MODE_CHAIN || mode == MODE_FLOW; }
+//   MODE_FLOW2  W=1 DNA single pairs: overlapping 64-column strips, DPP-add
+//               hand-offs, 11 instructions per step (sw_flow2.hip)
+enum : int { MODE_STRIP = 0, MODE_PAIRWG = 1, MODE_CHAIN = 2, MODE_DUO = 3, MODE_FLOW = 4, MODE_FLOW2 = 5 };
+inline bool grouped_mode(int mode) { return mode == MODE_CHAIN || mode == MODE_FLOW || mode == MODE_FLOW2; }
 
 // Host-side launch (sw_kernels.hip).
 struct LaunchCfg {
@@ -111,6 +114,19 @@ __host__ __device__ constexpr int flow_ring_rows(int W, int C) {
 // static LDS of sw_flow_kernel<W,C> (rings + sinks + words), rounded up
 __host__ __device__ constexpr int flow_static_lds(int W, int C) { return 3 * flow_ring_rows(W, C) * 8 + 4096; }
 __host__ __device__ constexpr int flow_stage_max(int W, int C) { return LDS_PER_CU - flow_static_lds(W, C); }
+
+// MODE_FLOW2 (sw_flow2.hip): strip s covers columns [63s, 63s + 64); the row
+// codes of the pair are staged in LDS (one byte per row, 64 rows of border in
+// front, a chunk of prefetch behind).
+__host__ __device__ constexpr int flow2_strips(int n) { return n <= 64 ? 1 : (n - 1 + 62) / 63; }
+__host__ __device__ constexpr int flow2_stage_bytes(int m, int C) {
+    return (64 + ((m + 64 + C - 1) / C + 1) * C + 8 + 15) & ~15;
+}
+__host__ __device__ constexpr int flow2_static_lds(int C) { return 4 * 256 * 8 + 4 * 64 * 8 + 4 * 64 * 4 + 64 + 0 * C; }
+__host__ __device__ constexpr int flow2_stage_max(int C) { return LDS_PER_CU - flow2_static_lds(C) - 256; }
+hipError_t launch_sw_flow2(const LaunchCfg& cfg, const KParams& kp, hipStream_t stream);
+int flow2_waves_per_cu(int C);
+bool flow2_variant_exists(int C);
 
 hipError_t launch_sw_strip(const LaunchCfg& cfg, const KParams& kp, hipStream_t stream);
 int kernel_waves_per_cu(const LaunchCfg& cfg);     // residency of the chosen variant

@@ -95,9 +95,16 @@ def test_config_c2_single_pair_65536(engine, golden):
     # symmetric: the transposed problem gives the same score
     assert engine.SmithWatermanScoreCUDA(b, a) == c["score"]
     # every grid organisation and a wider strip agree at full size
-    for mode in (0, 1, 2, 4):
+    for mode in (0, 1, 2, 4, 5):
         engine.set_option("mode", mode)
         assert engine.SmithWatermanScoreCUDA(a, b) == c["score"], mode
+    engine.set_option("mode", -1)
+    assert engine.last_stats()["mode"] == 5   # the automatic plan for C2 is the flow2 kernel
+    engine.set_option("mode", 5)
+    for C in (16, 64):
+        engine.set_option("C", C)
+        assert engine.SmithWatermanScoreCUDA(a, b) == c["score"], C
+    engine.set_option("C", 0)
     engine.set_option("mode", -1)
     engine.set_option("W", 4)
     assert engine.SmithWatermanScoreCUDA(a, b) == c["score"]
@@ -159,6 +166,57 @@ def test_every_variant_ragged(engine, oracle_mod):
                     for (a, b), e in list(zip(pairs, exp))[::4]:
                         assert engine.score(a, b, prm) == e, (W, C, force_bytes, mode, len(a), len(b))
                 engine.set_option("mode", -1)
+
+
+def test_flow2_ragged(engine, oracle_mod):
+    """The single-pair flow2 kernel (overlapping 64-column strips, W=1, DNA) on
+    ragged shapes around its 63-column stride, the 4-strip workgroups and the
+    chunk sizes; several pairs per launch; a one-workgroup grid; params whose
+    s + G_INIT leaves the signed byte fall back (auto) or fail (forced)."""
+    rng = np.random.default_rng(77)
+    shapes = [(1, 1), (1, 200), (200, 1), (63, 63), (64, 64), (65, 65), (126, 127), (127, 126), (128, 300),
+              (252, 253), (253, 252), (255, 1000), (256, 17), (505, 505), (1000, 64), (2017, 2100), (4096, 4000)]
+    pairs = []
+    for n, m in shapes:
+        a = _rand_dna(rng, n)
+        b = _rand_dna(rng, m)
+        if rng.random() < 0.5 and m > 10:
+            b = np.resize(a, m).copy()
+            mut = rng.random(m) < 0.05
+            b[mut] = _rand_dna(rng, int(mut.sum()))
+        pairs.append((a, b))
+    engine.set_option("orient", 1)   # keep (n, m) as given: seq1 across the lanes
+    try:
+        for prm in (engine.Params(), engine.Params(2, -3, 5, 2), engine.Params(1, -1, 3, 1), engine.Params(1, 0, 0, 0),
+                    engine.Params(60, -120, 67, 9)):
+            op = oracle_mod.Params(prm.match, prm.mismatch, prm.gap_init, prm.gap_ext)
+            exp = [oracle_mod.score_linear(a, b, op) for a, b in pairs]
+            engine.set_option("mode", 5)
+            for C in (16, 32, 64):
+                engine.set_option("C", C)
+                got = [engine.score(a, b, prm) for a, b in pairs]
+                assert got == exp, (C, prm)
+                assert engine.last_stats()["mode"] == 5
+                assert engine.score_batch(pairs, prm) == exp, (C, prm)
+            engine.set_option("C", 0)
+            engine.set_option("blocks", 1)
+            assert engine.score_batch(pairs, prm) == exp, prm
+            engine.set_option("blocks", 0)
+            engine.set_option("mode", -1)
+        # s + G_INIT > 127: the automatic plan uses another kernel, a forced flow2 reports an error
+        prm = engine.Params(100, -1, 40, 1)
+        a, b = pairs[-1]
+        e = oracle_mod.score_linear(a, b, oracle_mod.Params(100, -1, 40, 1))
+        assert engine.score(a, b, prm) == e
+        assert engine.last_stats()["mode"] != 5
+        engine.set_option("mode", 5)
+        with pytest.raises(RuntimeError):
+            engine.score(a, b, prm)
+    finally:
+        engine.set_option("mode", -1)
+        engine.set_option("C", 0)
+        engine.set_option("blocks", 0)
+        engine.set_option("orient", 0)
 
 
 def test_edges(engine, oracle_mod):

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
-"""Per-strip timeline of the flow kernel (mode 4) on one long pair.
+"""Per-strip timeline of the flow kernels (mode 4, or 5 = flow2) on one long pair.
 
-    python tools/trace_flow.py N C [W] [n_cols]
+    python tools/trace_flow.py N C [W] [n_cols] [mode]
 
 Each strip records s_memrealtime (100 MHz) at start, when its first inflow
 chunk arrived, and at the end, plus the number of failed progress polls.
@@ -23,14 +23,15 @@ def main():
     C = int(sys.argv[2]) if len(sys.argv) > 2 else 32
     W = int(sys.argv[3]) if len(sys.argv) > 3 else 1
     ncol = int(sys.argv[4]) if len(sys.argv) > 4 else N
+    mode = int(sys.argv[5]) if len(sys.argv) > 5 else 4
     torch.cuda.set_device(0)
     a, b = sw.gen_pair(N, N)
     a = a[:ncol]
     arena = torch.from_numpy(np.concatenate([a, b])).cuda()
     scores = torch.zeros(1, dtype=torch.int32, device="cuda")
-    strips = (ncol + 64 * W - 1) // (64 * W)
+    strips = (ncol + 64 * W - 1) // (64 * W) if mode != 5 else max(1, (ncol - 1 + 62) // 63)
     trace = torch.zeros(16 * strips, dtype=torch.int64, device="cuda")
-    sw.set_option("mode", 4)
+    sw.set_option("mode", mode)
     sw.set_option("W", W)
     sw.set_option("C", C)
     s = torch.cuda.current_stream()
