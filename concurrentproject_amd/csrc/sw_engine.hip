@@ -436,6 +436,9 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
         // pair-per-workgroup: one block per pair (grid-stride over pairs)
         const long long want = job.mode == MODE_STRIP ? (items + 3) / 4 : grouped_mode(job.mode) ? items : (long long)np;   // pairwg/duo: np workgroups
         blocks = std::min<long long>(want, cap);
+        // flow2 holds one workgroup per CU (its LDS size forces it); a grid larger than
+        // the CU count would only park extra workgroups until a CU frees up
+        if (job.mode == MODE_FLOW2) blocks = std::min<long long>(blocks, c->cus);
     }
     cfg.blocks = (int)std::max<long long>(1, blocks);
 

@@ -32,6 +32,7 @@
 // (sw_device.h).  Work items (groups of 4 strips) are claimed in order, so a
 // producer is always resident: no co-residency assumption, any grid size.
 // Every spin is bounded by s_memrealtime and reports ERR_TIMEOUT.
+#include <algorithm>
 #include <type_traits>
 
 #include "sw_device.h"
@@ -40,8 +41,17 @@ namespace swmi {
 namespace {
 
 constexpr int F2_R = 256;   // ring rows per link (power of two, >= 2C + 64)
+#ifndef SW_F2_GPREF
+#define SW_F2_GPREF 1       // cross-workgroup granules are loaded this many chunks ahead
+#endif
 #ifndef SW_F2_SPEC
-#define SW_F2_SPEC 2        // the next chunk's inflow is read after SW_F2_SPEC/4 of a chunk's steps
+#define SW_F2_SPEC 0        // >0: the next chunk's inflow is read speculatively after SW_F2_SPEC/4 of a chunk
+#endif
+#ifndef SW_F2_GPOS
+#define SW_F2_GPOS 2        // chunk c+SW_F2_GPREF's granules are loaded after SW_F2_GPOS/4 of chunk c's steps
+#endif
+#ifndef SW_F2_HALFPUB
+#define SW_F2_HALFPUB 1     // workgroup-edge strips publish granules every half chunk
 #endif
 
 constexpr int DPP_WAVE_SHL1 = 0x130;
@@ -56,6 +66,14 @@ __device__ __forceinline__ int dpp_add_shr1_tied(int old, int src, int k, int af
     asm("v_add_u32_dpp %0, %1, %2 wave_shr:1 row_mask:0xf bank_mask:0xf ; dep %3"
         : "+v"(old) : "v"(src), "v"(k), "v"(after));
     return old;
+}
+
+// s_memrealtime with its wait inside the asm: nothing SMEM stays outstanding, so
+// the compiler's LDS wait counts around a stamp stay exact (tools only)
+__device__ __forceinline__ long long realtime_waited() {
+    long long t;
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    return t;
 }
 
 // gfx950 LDS serves unaligned dword reads (ds_read_b32 at any byte address)
@@ -125,6 +143,7 @@ __global__ void __launch_bounds__(256) sw_flow2_kernel(KParams kp) {
         const long long t_start = (long long)__builtin_amdgcn_s_memrealtime();
         bool failed = false;
         long long t_first = t_start;
+        int nslow = 0;   // chunks whose inflow took the slow path (trace only)
         long long tl[5] = {0, 0, 0, 0, 0};   // SW_TIMELINE: wall clock at chunks 1, 2, 3, 50, 1000
         int H = 0, E = 0, fh = -ge, hgO = -go, L0 = -go, ehP = -ge, M = 0;
         int IOH = -go, IOE = -ge;                 // rotating I/O registers (see the step)
@@ -143,14 +162,31 @@ __global__ void __launch_bounds__(256) sw_flow2_kernel(KParams kp) {
 
         auto flow_loop = [&](auto in_c, auto out_c) __attribute__((always_inline)) {
             constexpr int IN = decltype(in_c)::value, OUT = decltype(out_c)::value;
-            u32x4 gpre = u32x4{0u, 0u, 0u, 0u};
-            if constexpr (IN == FLOW_GRANULE) gpre = fetch_granules<C>(in_rsrc, 0, lane, m);
+            // granule prefetch queue: gq[i] holds the loads for chunk c + i (issued SW_F2_GPREF chunks ahead)
+            u32x4 gq[SW_F2_GPREF];
+#pragma unroll
+            for (int i = 0; i < SW_F2_GPREF; ++i)
+                gq[i] = IN == FLOW_GRANULE ? fetch_granules<C>(in_rsrc, i * C, lane, m) : u32x4{0u, 0u, 0u, 0u};
             unsigned D[C / 4];
 #pragma unroll
             for (int u = 0; u < C / 4; ++u) D[u] = load_u32_unaligned(code_base + 4 * u);
             int cons_seen = 0;
             int spec_avail = -1;                 // progress word read with spec_v (-1: none)
             int2 spec_v = make_int2(0, 0);
+            // granule outflow at step k0 (chunk start, or mid-chunk with SW_F2_HALFPUB):
+            // lane L >= 64 - C holds row k0 - 128 + L; with half-chunk publishing only
+            // lanes >= 64 - C/2 are new
+            auto publish_granules_half = [&](const int k0) __attribute__((always_inline)) {
+                const int row_out = k0 - 128 + lane;
+                constexpr int LO = SW_F2_HALFPUB ? 64 - C / 2 : 64 - C;
+                const bool st = lane >= LO && row_out >= 0 && row_out < m;
+                u32x4 g;
+                g.x = kp.epoch;
+                g.y = (unsigned)IOH;
+                g.z = (unsigned)IOE;
+                g.w = granule_chk(kp.epoch, IOH, IOE, row_out);
+                __builtin_amdgcn_raw_buffer_store_b128(g, out_rsrc, st ? (unsigned)row_out * 16u : OOR, 0, AUX_SC1);
+            };
             // ---- publish the last chunk's outflow: lane L >= 64 - C holds row k0 - 128 + L
             auto publish = [&](const int k0) __attribute__((always_inline)) {
                 const int row_out = k0 - 128 + lane;
@@ -173,49 +209,73 @@ __global__ void __launch_bounds__(256) sw_flow2_kernel(KParams kp) {
                     compiler_fence();
                     *prod_out = max(0, k0 - 64);   // after the ring writes (in-order DS)
                 } else if constexpr (OUT == FLOW_GRANULE) {
-                    const bool st = lane >= 64 - C && row_out >= 0 && row_out < m;
-                    u32x4 g;
-                    g.x = kp.epoch;
-                    g.y = (unsigned)IOH;
-                    g.z = (unsigned)IOE;
-                    g.w = granule_chk(kp.epoch, IOH, IOE, row_out);
-                    __builtin_amdgcn_raw_buffer_store_b128(g, out_rsrc, st ? (unsigned)row_out * 16u : OOR, 0, AUX_SC1);
+                    publish_granules_half(k0);
                 }
             };
             for (int c = 0; c < nloc; ++c) {
                 const int k0 = c * C;
 #ifdef SW_TIMELINE
-                if (c == 1 || c == 2 || c == 3 || c == 50 || c == 1000) {
-                    const long long now = (long long)__builtin_amdgcn_s_memrealtime();
-                    tl[c == 1 ? 0 : c == 2 ? 1 : c == 3 ? 2 : c == 50 ? 3 : 4] = now;
-                }
+                if (c == 1 || c == 2 || c == 3 || c == 50 || c == 1000)
+                    tl[c == 1 ? 0 : c == 2 ? 1 : c == 3 ? 2 : c == 50 ? 3 : 4] = realtime_waited();
 #endif
                 // ---- inflow rows [k0, k0 + C), for lanes [0, C) of the I/O registers
                 int newH, newE;
                 if constexpr (IN == FLOW_GRANULE) {
-                    u32x4 g = gpre;
+                    u32x4 g = gq[0];
+                    if (kp.trace != nullptr) {   // tools: count chunks whose granules were not there yet
+                        const int row = k0 + lane;
+                        const bool need = lane < C && row < m;
+                        nslow += __all((!need) | granule_ok(g, kp.epoch, row)) ? 0 : 1;
+                    }
                     await_granules<C>(kp, in_rsrc, g, k0, lane, m, strip, failed);
-                    gpre = fetch_granules<C>(in_rsrc, k0 + C, lane, m);
+#pragma unroll
+                    for (int i = 0; i + 1 < SW_F2_GPREF; ++i) gq[i] = gq[i + 1];
+                    if constexpr (SW_F2_GPOS == 0)
+                        gq[SW_F2_GPREF - 1] = fetch_granules<C>(in_rsrc, k0 + SW_F2_GPREF * C, lane, m);
                     const bool live = k0 + lane < m;
                     newH = live ? (int)g.y : -go;
                     newE = live ? (int)g.z : -ge;
                 } else if constexpr (IN == FLOW_LDS) {
-                    // the rows were read speculatively during the last chunk, behind a read
-                    // of the progress word; only if that word did not cover them, poll and re-read
                     const int need = min(k0 + C, m);
-                    int2 v = spec_v;
-                    if (__builtin_amdgcn_readfirstlane(spec_avail) < need) {
-                        int avail = __builtin_amdgcn_readfirstlane(lds_load(&prod[wave - 1]));
-                        while (avail < need) {
-                            __builtin_amdgcn_s_sleep(SW_SPIN_SLEEP);
-                            avail = __builtin_amdgcn_readfirstlane(lds_load(&prod[wave - 1]));
-                            if ((long long)__builtin_amdgcn_s_memrealtime() - t_start > kp.timeout_ticks) {
-                                failed = true;
-                                break;
+                    int2 v;
+                    if constexpr (SW_F2_SPEC > 0) {
+                        // the rows were read speculatively during the last chunk, behind a read
+                        // of the progress word; only if that word did not cover them, poll and re-read
+                        v = spec_v;
+                        if (__builtin_amdgcn_readfirstlane(spec_avail) < need) {
+                            ++nslow;
+                            int avail = __builtin_amdgcn_readfirstlane(lds_load(&prod[wave - 1]));
+                            while (avail < need) {
+                                __builtin_amdgcn_s_sleep(SW_SPIN_SLEEP);
+                                avail = __builtin_amdgcn_readfirstlane(lds_load(&prod[wave - 1]));
+                                if ((long long)__builtin_amdgcn_s_memrealtime() - t_start > kp.timeout_ticks) {
+                                    failed = true;
+                                    break;
+                                }
                             }
+                            compiler_fence();
+                            v = in_ring[(k0 + (lane & (C - 1))) & (R - 1)];
                         }
+                    } else {
+                        // the progress word and the chunk's rows in one LDS round trip (DS ops
+                        // of a wave execute in order: rows read after a word that covers them
+                        // are complete); re-read both until the word covers the chunk
+                        int avail = lds_load(&prod[wave - 1]);
                         compiler_fence();
                         v = in_ring[(k0 + (lane & (C - 1))) & (R - 1)];
+                        if (__builtin_amdgcn_readfirstlane(avail) < need) {
+                            ++nslow;
+                            do {
+                                __builtin_amdgcn_s_sleep(SW_SPIN_SLEEP);
+                                avail = lds_load(&prod[wave - 1]);
+                                compiler_fence();
+                                v = in_ring[(k0 + (lane & (C - 1))) & (R - 1)];
+                                if ((long long)__builtin_amdgcn_s_memrealtime() - t_start > kp.timeout_ticks) {
+                                    failed = true;
+                                    break;
+                                }
+                            } while (__builtin_amdgcn_readfirstlane(avail) < need);
+                        }
                     }
                     newH = v.x;
                     newE = v.y;
@@ -238,14 +298,21 @@ __global__ void __launch_bounds__(256) sw_flow2_kernel(KParams kp) {
                     *cons_out = k0 + C;   // after the ring read (DS ops execute in order)
                 }
 #ifdef SW_TIMELINE
-                if (c == 0) t_first = (long long)__builtin_amdgcn_s_memrealtime();
+                if (c == 0) t_first = realtime_waited();
 #endif
 #pragma unroll
                 for (int u = 0; u < C / 4; ++u) D[u] = load_u32_unaligned(code_base + k0 + C + 4 * u);
                 // ---- C anti-diagonal steps
 #pragma unroll
                 for (int j = 0; j < C; j += 4) {
-                    if constexpr (IN == FLOW_LDS) {
+                    if constexpr (IN == FLOW_GRANULE && SW_F2_GPOS > 0) {
+                        if (j == SW_F2_GPOS * C / 4) gq[SW_F2_GPREF - 1] = fetch_granules<C>(in_rsrc, k0 + SW_F2_GPREF * C, lane, m);
+                    }
+                    if constexpr (OUT == FLOW_GRANULE && SW_F2_HALFPUB) {
+                        // lanes [64 - C/2, 64) hold this chunk's first C/2 outflow rows
+                        if (j == C / 2) publish_granules_half(k0 + C / 2);
+                    }
+                    if constexpr (IN == FLOW_LDS && SW_F2_SPEC > 0) {
                         if (j == SW_F2_SPEC * C / 4) {   // speculative read of the next chunk's inflow
                             spec_avail = lds_load(&prod[wave - 1]);
                             compiler_fence();
@@ -299,6 +366,7 @@ __global__ void __launch_bounds__(256) sw_flow2_kernel(KParams kp) {
             unsigned long long* t = kp.trace + 16ull * (unsigned)strip;
             t[0] = (unsigned long long)t_start;
             t[1] = (unsigned long long)t_first;
+            t[3] = (unsigned long long)nslow;
             t[2] = (unsigned long long)__builtin_amdgcn_s_memrealtime();
             t[7] = (unsigned long long)nloc;
             for (int q = 0; q < 5; ++q) t[8 + q] = (unsigned long long)tl[q];
@@ -315,7 +383,10 @@ __global__ void __launch_bounds__(256) sw_flow2_kernel(KParams kp) {
 
 template <int C>
 hipError_t launch_c(const LaunchCfg& cfg, const KParams& kp, hipStream_t s) {
-    const int dyn = flow2_stage_bytes(cfg.max_m, C);
+    // at least half the CU's LDS: one workgroup per CU, so no strip ever shares a
+    // SIMD with another (a co-resident waiting workgroup's polls steal issue slots
+    // from a strip on the critical path)
+    const int dyn = std::max(flow2_stage_bytes(cfg.max_m, C), LDS_PER_CU / 2 + 1024 - flow2_static_lds(C));
     if (dyn > flow2_stage_max(C)) return hipErrorInvalidValue;
     static int dyn_set = 0;   // raise the dynamic-LDS limit once per variant
     if (dyn > 64 * 1024 && dyn_set == 0) {

@@ -84,6 +84,15 @@ def main():
         out["first_to_c1_ns_median"] = float(np.median(tl[:, 0] - first))
         for k in sorted({k for k in (0, 1, 2, 3, 4, 5, 500, strips - 1) if k < strips}):
             print("TL", k, [int(x) for x in tl[k]], int(first[k]))
+    d_end = np.diff(end)
+    out["lag_end_ns_median"] = float(np.median(d_end)) if d_end.size else None
+    out["lag_end_ns_ingroup"] = float(np.median(d_end[ingroup])) if d_end.size else None
+    out["lag_end_ns_crossgroup"] = float(np.median(d_end[~ingroup])) if (~ingroup).any() else None
+    out["strip0_run_ns_per_step"] = float(end[0] - start[0]) / steps
+    sl = spins[1:]
+    xg = np.array([(k + 1) % 4 == 0 for k in range(strips - 1)], dtype=bool)
+    out["slow_chunks_ingroup_mean"] = float(sl[~xg].mean()) if sl.size else None
+    out["slow_chunks_crossgroup_mean"] = float(sl[xg].mean()) if xg.any() else None
     print(json.dumps(out))
     for k in list(range(0, 9)) + list(range(strips - 5, strips)):
         print(k, int(start[k]), int(first[k]), int(end[k]), int(spins[k]), round(run_ns[k] / steps, 2))
