@@ -22,7 +22,8 @@ __all__ = [
     "Params", "lib", "build", "SequentialSmithWatermanScoreGPU", "SmithWatermanLazyGPU",
     "SmithWatermanScoreCUDA", "SmithDiagonalGPU", "score", "score_batch", "score_batch_device",
     "set_params", "get_params", "set_option", "get_option", "last_stats", "gen_pair", "gen_batch",
-    "SwError", "LIB_PATH",
+    "SwError", "LIB_PATH", "SW_FLAG_DNA", "SW_FLAG_BYTES", "slab_bounds", "SlabBuffer", "slab_alloc",
+    "ipc_open", "ipc_close", "score_slab_device",
 ]
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -104,6 +105,19 @@ def lib() -> ctypes.CDLL:
     L.sw_version.restype = i
     L.sw_gen_pair.argtypes = [ctypes.c_uint64, i, u8p, u8p]
     L.sw_gen_batch.argtypes = [ctypes.c_uint64, i, i, u8p]
+    vp = ctypes.c_void_p
+    L.sw_slab_bounds.argtypes = [ctypes.c_longlong, i, i, i, ctypes.POINTER(ctypes.c_longlong)]
+    L.sw_slab_bounds.restype = i
+    L.sw_score_slab_device.argtypes = [vp, ctypes.c_int64, i, ctypes.c_int64, i, vp, vp, ctypes.c_uint, vp, i, vp]
+    L.sw_score_slab_device.restype = i
+    L.sw_slab_alloc.argtypes = [i, ctypes.POINTER(vp), ctypes.c_char_p]
+    L.sw_slab_alloc.restype = i
+    L.sw_slab_free.argtypes = [vp]
+    L.sw_slab_free.restype = i
+    L.sw_ipc_open.argtypes = [ctypes.c_char_p, ctypes.POINTER(vp)]
+    L.sw_ipc_open.restype = i
+    L.sw_ipc_close.argtypes = [vp]
+    L.sw_ipc_close.restype = i
     _lib = L
     return L
 
@@ -203,6 +217,64 @@ def score_batch_device(d_arena_ptr: int, a_off, alen, b_off, blen, d_scores_ptr:
 
 def stream_status(stream: int | None = None) -> None:
     _check(lib().sw_stream_status(ctypes.c_void_p(stream) if stream else None))
+
+
+# ---- one pair in column slabs across GPUs (dist.ColumnSlabs drives these) -----------------
+
+SW_IPC_HANDLE_BYTES = 64
+
+
+def slab_bounds(n: int, m: int, nslabs: int, flags: int) -> list:
+    """Column bounds [b_0 = 0, ..., b_nslabs = n] of nslabs slabs; every slab but the
+    last is a multiple of the planned kernel's column quantum (63 or 64*W)."""
+    out = (ctypes.c_longlong * (nslabs + 1))()
+    _check(lib().sw_slab_bounds(int(n), int(m), int(nslabs), int(flags), out))
+    return [int(x) for x in out]
+
+
+class SlabBuffer:
+    """A slab's inflow edge: m zeroed 16-byte granules in device memory, and the
+    IPC handle under which the rank that writes it maps it."""
+
+    def __init__(self, m: int):
+        p = ctypes.c_void_p()
+        h = ctypes.create_string_buffer(SW_IPC_HANDLE_BYTES)
+        kind = _check(lib().sw_slab_alloc(int(m), ctypes.byref(p), h))
+        self.ptr = int(p.value)
+        self.handle = h.raw
+        self.fine_grained = kind == 1
+        self.m = m
+
+    def free(self) -> None:
+        if self.ptr:
+            _check(lib().sw_slab_free(ctypes.c_void_p(self.ptr)))
+            self.ptr = 0
+
+
+def slab_alloc(m: int) -> SlabBuffer:
+    return SlabBuffer(m)
+
+
+def ipc_open(handle: bytes) -> int:
+    """Map another process's slab buffer (hipIpcOpenMemHandle); returns its device address here."""
+    p = ctypes.c_void_p()
+    _check(lib().sw_ipc_open(handle, ctypes.byref(p)))
+    return int(p.value)
+
+
+def ipc_close(ptr: int) -> None:
+    if ptr:
+        _check(lib().sw_ipc_close(ctypes.c_void_p(ptr)))
+
+
+def score_slab_device(d_arena_ptr: int, col_off: int, n: int, row_off: int, m: int, d_inflow: int,
+                      d_outflow: int, epoch: int, d_score_ptr: int, flags: int, stream: int | None = None) -> None:
+    """One column slab (sw_score_slab_device): *d_score = max H over its cells."""
+    _check(lib().sw_score_slab_device(ctypes.c_void_p(d_arena_ptr), int(col_off), int(n), int(row_off), int(m),
+                                      ctypes.c_void_p(d_inflow) if d_inflow else None,
+                                      ctypes.c_void_p(d_outflow) if d_outflow else None, int(epoch),
+                                      ctypes.c_void_p(d_score_ptr), int(flags),
+                                      ctypes.c_void_p(stream) if stream else None))
 
 
 def set_params(p: Params) -> None:

@@ -75,6 +75,24 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t bnd_rsrc(const KParams& kp, co
     return __builtin_amdgcn_make_buffer_rsrc(base, 0, pd.m * 16, RSRC_FLAGS);
 }
 
+// Grouped modes: granule buffer of group boundary b (between groups b and b+1).
+// b = -1 is the slab inflow and b = ngroups-1 the slab outflow of a multi-GPU
+// column slab (KParams::slab_in / slab_out); without a slab those roles never
+// reach a granule load or store, and the resource points at the arena.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t group_rsrc(const KParams& kp, const PairDesc& pd, int b,
+                                                             int ngroups) {
+    Granule* base = kp.bnd + pd.bnd_off + (uint64_t)(b < 0 ? 0 : b) * (uint64_t)pd.m;
+    if (b < 0 && kp.slab_in != nullptr) base = kp.slab_in;
+    if (b >= ngroups - 1 && kp.slab_out != nullptr) base = kp.slab_out;
+    return __builtin_amdgcn_make_buffer_rsrc(base, 0, pd.m * 16, RSRC_FLAGS);
+}
+// epoch of the granules crossing group boundary b (slab edges carry the ranks' common epoch)
+__device__ __forceinline__ unsigned group_epoch(const KParams& kp, int b, int ngroups) {
+    if (b < 0 && kp.slab_in != nullptr) return kp.slab_epoch;
+    if (b >= ngroups - 1 && kp.slab_out != nullptr) return kp.slab_epoch;
+    return kp.epoch;
+}
+
 __device__ __forceinline__ bool granule_ok(const u32x4& g, unsigned epoch, int row) {
     // bitwise, not short-circuit: no exec-mask branch per lane
     return (g.x == epoch) & (g.w == granule_chk(epoch, (int)g.y, (int)g.z, row));
@@ -116,16 +134,16 @@ __device__ __noinline__ AwaitRes await_slow(__amdgpu_buffer_rsrc_t in_rsrc, u32x
     }
 }
 
-// Wait until the granules of rows [k0, k0+C) are all published (bounded spin).
+// Wait until the granules of rows [k0, k0+C) are all published with `epoch` (bounded spin).
 template <int C>
 __device__ __forceinline__ void await_granules(const KParams& kp, const __amdgpu_buffer_rsrc_t in_rsrc, u32x4& g,
-                                               int k0, int lane, int m, int strip, bool& failed) {
+                                               int k0, int lane, int m, int strip, bool& failed, unsigned epoch) {
     if (failed) return;
     const int row = k0 + lane;
     const bool need = lane < C && row >= 0 && row < m;
-    const bool ok = (!need) | granule_ok(g, kp.epoch, row);
+    const bool ok = (!need) | granule_ok(g, epoch, row);
     if (__all(ok)) return;
-    const AwaitRes r = await_slow(in_rsrc, g, row, need, kp.epoch, kp.timeout_ticks, kp.ctrl, strip, lane);
+    const AwaitRes r = await_slow(in_rsrc, g, row, need, epoch, kp.timeout_ticks, kp.ctrl, strip, lane);
     g = r.g;
     failed = r.failed != 0;
 }

@@ -235,11 +235,11 @@ int pick_mode(const std::vector<PairDesc>& pairs, bool single) {
     return st[st.size() / 2] >= 4 ? MODE_PAIRWG : MODE_STRIP;
 }
 
-void plan(Job& job, int W, int C, bool single) {
+void plan(Job& job, int W, int C, bool single, int mode = -1) {
     job.W = W;
     job.C = C;
     for (auto& d : job.pairs) d.strips = (d.n + 64 * W - 1) / (64 * W);
-    job.mode = pick_mode(job.pairs, single);
+    job.mode = mode >= 0 ? mode : pick_mode(job.pairs, single);
     job.item_base.assign(job.pairs.size() + 1, 0);
     uint64_t g = 0;
     long long cells = 0;
@@ -366,6 +366,44 @@ int finalize_mode(Job& job, const Params& prm) {
     return 0;
 }
 
+// Plan of ONE column slab of a pair split across GPUs.
+// sw_score_slab_device and sw_slab_bounds share it, so the bounds a rank
+// computes are cut for exactly the kernel every rank runs.  W = 1 unless
+// forced: the narrowest strips give the shortest wavefront through the ranks.
+// Returns the column quantum a slab with an outflow edge must be a multiple
+// of -- 63 for flow2 (its last strip's lane 62 is then the slab's last column),
+// 64*W for chain / flow (no dead columns at the edge) -- or -1.
+int plan_slab(Job& job, int n, int m, bool dna, const Params& prm) {
+    job.pairs.assign(1, PairDesc{});
+    PairDesc& d = job.pairs[0];
+    d.n = n;
+    d.m = m;
+    d.out_idx = 0;
+    job.dna = dna;
+    const long long fw = g_opt_W.load();
+    const int W = fw ? (int)fw : 1;
+    const long long fm = g_opt_mode.load();
+    plan(job, W, pick_C(W), true, fm >= 0 ? (int)fm : MODE_CHAIN);
+    if (finalize_mode(job, prm)) return -1;
+    if (!grouped_mode(job.mode)) {
+        set_err("a column slab needs a grouped kernel (chain, flow or flow2), not mode %d", job.mode);
+        return -1;
+    }
+    return job.mode == MODE_FLOW2 ? 63 : 64 * job.W;
+}
+
+// Alphabet of a slab call: stated by the caller, never scanned, because every
+// rank must plan the same kernel family for its slab.
+int slab_dna(int flags, bool* dna) {
+    const bool bytes = (flags & SW_FLAG_BYTES) || g_opt_bytes.load();
+    if (!bytes && !(flags & SW_FLAG_DNA)) {
+        set_err("column slabs need SW_FLAG_DNA or SW_FLAG_BYTES: every rank must plan the same kernel");
+        return -1;
+    }
+    *dna = !bytes;
+    return 0;
+}
+
 void profile_words(const Params& p, unsigned out[4]) {
     for (int q = 0; q < 4; ++q) {
         unsigned w = 0;
@@ -387,9 +425,17 @@ int waves_per_cu(Ctx* c, const LaunchCfg& cfg) {
     return w;
 }
 
+// Edges of a column slab (sw_score_slab_device): granule buffers of the left
+// and right slab boundaries and the epoch every rank tags them with.
+struct SlabEdge {
+    Granule* in;
+    Granule* out;
+    unsigned epoch;
+};
+
 // Enqueue the launch for a planned job whose sequences are in `d_seq`.
 int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int* d_scores, int nscores,
-            hipStream_t s, bool time_kernel) {
+            hipStream_t s, bool time_kernel, const SlabEdge* edge = nullptr) {
     if (job.mode == MODE_FLOW2 ? !flow2_variant_exists(job.C) : !variant_exists(job.W, job.C)) {
         set_err("no kernel variant for W=%d C=%d", job.W, job.C);
         return -1;
@@ -471,6 +517,11 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
     }
     kp.timeout_ticks = g_opt_timeout.load() * 100000000LL;   // s_memrealtime: 100 MHz
     kp.trace = reinterpret_cast<unsigned long long*>(g_opt_trace.load());
+    if (edge) {
+        kp.slab_in = edge->in;
+        kp.slab_out = edge->out;
+        kp.slab_epoch = edge->epoch;
+    }
 
     if (time_kernel) HIPCHK(hipEventRecord(c->ev0, s));
     HIPCHK(job.mode == MODE_FLOW2 ? launch_sw_flow2(cfg, kp, s) : launch_sw_strip(cfg, kp, s));
@@ -758,6 +809,133 @@ int sw_score_batch_device(const unsigned char* d_arena, const int64_t* a_off, co
         t_stats.kernel_ms = ms;
     }
     t_stats.total_ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return 0;
+}
+
+int sw_slab_bounds(long long n, int m, int nslabs, int flags, long long* bounds) {
+    if (n <= 0 || n > (1LL << 30) || m <= 0 || nslabs <= 0 || !bounds) {
+        set_err("sw_slab_bounds: invalid arguments");
+        return -1;
+    }
+    bool dna = true;
+    if (slab_dna(flags, &dna)) return -1;
+    Job job;
+    const int q = plan_slab(job, (int)n, m, dna, current_params());   // the quantum does not depend on n
+    if (q < 0) return -1;
+    const long long per = n / nslabs / q * q;
+    if (nslabs > 1 && per == 0) {
+        set_err("%lld columns cannot be cut into %d slabs of a multiple of %d columns", n, nslabs, q);
+        return -1;
+    }
+    for (int r = 0; r < nslabs; ++r) bounds[r] = per * r;   // the last slab takes the remainder
+    bounds[nslabs] = n;
+    return q;
+}
+
+int sw_score_slab_device(const unsigned char* d_arena, int64_t col_off, int n, int64_t row_off, int m,
+                         void* d_inflow, void* d_outflow, unsigned epoch, int* d_score, int flags, void* stream) {
+    const auto t0 = std::chrono::steady_clock::now();
+    if (!d_arena || !d_score || n <= 0 || m <= 0 || col_off < 0 || row_off < 0) {
+        set_err("sw_score_slab_device: invalid arguments");
+        return -1;
+    }
+    if ((d_inflow || d_outflow) && epoch == 0) {
+        set_err("sw_score_slab_device: epoch 0 is the tag of a never-written granule");
+        return -1;
+    }
+    bool dna = true;
+    if (slab_dna(flags, &dna)) return -1;
+    const Params prm = current_params();
+    if (!params_ok(prm)) return -1;
+    // H of any cell is at most MATCH * (its row), whatever the slab's column range
+    if ((long long)m * std::max(prm.match, 1) >= (1LL << 28)) {
+        set_err("slab: rows * MATCH >= 2^28 exceeds the int32 engine");
+        return -1;
+    }
+    Ctx* c = get_ctx();
+    if (!c) return -1;
+    hipStream_t s = stream ? (hipStream_t)stream : c->own;
+    if (c->last && c->last != s) HIPCHK(hipStreamSynchronize(c->last));
+    Job job;
+    const int q = plan_slab(job, n, m, dna, prm);
+    if (q < 0) return -1;
+    if (d_outflow && n % q != 0) {
+        set_err("a slab with an outflow edge must be a multiple of %d columns (sw_slab_bounds), got %d", q, n);
+        return -1;
+    }
+    job.pairs[0].col_off = (uint64_t)col_off;
+    job.pairs[0].row_off = (uint64_t)row_off;
+    const SlabEdge edge{static_cast<Granule*>(d_inflow), static_cast<Granule*>(d_outflow), epoch};
+    if (enqueue(c, job, prm, d_arena, d_score, 1, s, !stream, &edge)) return -1;
+    if (!stream) {
+        if (check_ctrl(c, s)) return -1;
+        float ms = 0.f;
+        HIPCHK(hipEventElapsedTime(&ms, c->ev0, c->ev1));
+        t_stats.kernel_ms = ms;
+    }
+    t_stats.total_ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return 0;
+}
+
+int sw_slab_alloc(int m, void** d_buf, void* ipc_handle) {
+    if (m <= 0 || !d_buf) {
+        set_err("sw_slab_alloc: invalid arguments");
+        return -1;
+    }
+    const size_t bytes = (size_t)m * sizeof(Granule);
+    // fine-grained: coherent for a peer GPU's writes while the consuming kernel
+    // polls; plain device memory if the driver cannot export fine-grained memory
+    for (int kind = 1; kind <= 2; ++kind) {
+        void* p = nullptr;
+        const hipError_t e = kind == 1 ? hipExtMallocWithFlags(&p, bytes, hipDeviceMallocFinegrained)
+                                       : hipMalloc(&p, bytes);
+        if (e != hipSuccess) {
+            (void)hipGetLastError();
+            if (kind == 2) {
+                set_err("sw_slab_alloc: %s", hipGetErrorString(e));
+                return -1;
+            }
+            continue;
+        }
+        HIPCHK(hipMemset(p, 0, bytes));   // tag 0: no granule is valid before its epoch is written
+        if (ipc_handle) {
+            hipIpcMemHandle_t h;
+            const hipError_t ei = hipIpcGetMemHandle(&h, p);
+            if (ei != hipSuccess) {
+                (void)hipGetLastError();
+                (void)hipFree(p);
+                if (kind == 2) {
+                    set_err("hipIpcGetMemHandle failed: %s", hipGetErrorString(ei));
+                    return -1;
+                }
+                continue;
+            }
+            std::memcpy(ipc_handle, &h, sizeof h);
+        }
+        *d_buf = p;
+        return kind;
+    }
+    return -1;
+}
+
+int sw_slab_free(void* d_buf) {
+    if (d_buf) HIPCHK(hipFree(d_buf));
+    return 0;
+}
+
+int sw_ipc_open(const void* ipc_handle, void** d_ptr) {
+    if (!ipc_handle || !d_ptr) {
+        set_err("sw_ipc_open: invalid arguments");
+        return -1;
+    }
+    hipIpcMemHandle_t h;
+    std::memcpy(&h, ipc_handle, sizeof h);
+    HIPCHK(hipIpcOpenMemHandle(d_ptr, h, hipIpcMemLazyEnablePeerAccess));
+    return 0;
+}
+
+int sw_ipc_close(void* d_ptr) {
+    if (d_ptr) HIPCHK(hipIpcCloseMemHandle(d_ptr));
     return 0;
 }
 

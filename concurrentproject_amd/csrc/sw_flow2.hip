@@ -136,10 +136,16 @@ __global__ void __launch_bounds__(256) sw_flow2_kernel(KParams kp) {
         if (strip >= pd.strips) continue;
         const int col = 63 * strip + lane;
         const unsigned prof = col < pd.n ? kp.prof2[dna_code(kp.seq[pd.col_off + col])] : 0x80808080u;
-        const int in_kind = wave > 0 ? FLOW_LDS : strip > 0 ? FLOW_GRANULE : FLOW_NONE;
-        const int out_kind = strip + 1 >= pd.strips ? FLOW_NONE : wave < 3 ? FLOW_LDS : FLOW_GRANULE;
-        const __amdgpu_buffer_rsrc_t in_rsrc = bnd_rsrc(kp, pd, group - 1);
-        const __amdgpu_buffer_rsrc_t out_rsrc = bnd_rsrc(kp, pd, group);
+        // a multi-GPU column slab: the first strip takes the previous slab's edge, the
+        // last one hands its lane-62 column (the next slab's left neighbour) on
+        const int ngroups = (pd.strips + 3) / 4;
+        const int in_kind = wave > 0 ? FLOW_LDS : (strip > 0 || kp.slab_in != nullptr) ? FLOW_GRANULE : FLOW_NONE;
+        const int out_kind = strip + 1 >= pd.strips ? (kp.slab_out != nullptr ? FLOW_GRANULE : FLOW_NONE)
+                             : wave < 3           ? FLOW_LDS
+                                                  : FLOW_GRANULE;
+        const __amdgpu_buffer_rsrc_t in_rsrc = group_rsrc(kp, pd, group - 1, ngroups);
+        const __amdgpu_buffer_rsrc_t out_rsrc = group_rsrc(kp, pd, group, ngroups);
+        const unsigned ep_in = group_epoch(kp, group - 1, ngroups), ep_out = group_epoch(kp, group, ngroups);
         const long long t_start = (long long)__builtin_amdgcn_s_memrealtime();
         bool failed = false;
         long long t_first = t_start;
@@ -181,10 +187,10 @@ __global__ void __launch_bounds__(256) sw_flow2_kernel(KParams kp) {
                 constexpr int LO = SW_F2_HALFPUB ? 64 - C / 2 : 64 - C;
                 const bool st = lane >= LO && row_out >= 0 && row_out < m;
                 u32x4 g;
-                g.x = kp.epoch;
+                g.x = ep_out;
                 g.y = (unsigned)IOH;
                 g.z = (unsigned)IOE;
-                g.w = granule_chk(kp.epoch, IOH, IOE, row_out);
+                g.w = granule_chk(ep_out, IOH, IOE, row_out);
                 __builtin_amdgcn_raw_buffer_store_b128(g, out_rsrc, st ? (unsigned)row_out * 16u : OOR, 0, AUX_SC1);
             };
             // ---- publish the last chunk's outflow: lane L >= 64 - C holds row k0 - 128 + L
@@ -225,9 +231,9 @@ __global__ void __launch_bounds__(256) sw_flow2_kernel(KParams kp) {
                     if (kp.trace != nullptr) {   // tools: count chunks whose granules were not there yet
                         const int row = k0 + lane;
                         const bool need = lane < C && row < m;
-                        nslow += __all((!need) | granule_ok(g, kp.epoch, row)) ? 0 : 1;
+                        nslow += __all((!need) | granule_ok(g, ep_in, row)) ? 0 : 1;
                     }
-                    await_granules<C>(kp, in_rsrc, g, k0, lane, m, strip, failed);
+                    await_granules<C>(kp, in_rsrc, g, k0, lane, m, strip, failed, ep_in);
 #pragma unroll
                     for (int i = 0; i + 1 < SW_F2_GPREF; ++i) gq[i] = gq[i + 1];
                     if constexpr (SW_F2_GPOS == 0)
@@ -357,9 +363,11 @@ __global__ void __launch_bounds__(256) sw_flow2_kernel(KParams kp) {
             else flow_loop(I2{}, I0{});
         } else if (in_kind == FLOW_GRANULE) {
             if (out_kind == FLOW_LDS) flow_loop(I1{}, I2{});
+            else if (out_kind == FLOW_GRANULE) flow_loop(I1{}, I1{});   // one-strip group between slab edges
             else flow_loop(I1{}, I0{});
         } else {
             if (out_kind == FLOW_LDS) flow_loop(I0{}, I2{});
+            else if (out_kind == FLOW_GRANULE) flow_loop(I0{}, I1{});   // a one-strip first slab
             else flow_loop(I0{}, I0{});
         }
         if (kp.trace != nullptr && lane == 0) {

@@ -79,6 +79,14 @@ struct KParams {
     const DuoDesc* duos;          // duo mode: nduos descriptors (npairs counts duos)
     long long timeout_ticks;      // s_memrealtime ticks (100 MHz) before a spin gives up
     unsigned long long* trace;    // optional (tools/trace_flow.py): per-strip timestamps, else null
+    // Column slab of a pair split across GPUs (grouped modes, one pair per launch):
+    // the first group's inflow comes from slab_in (the previous slab's last
+    // column, written by the previous GPU over xGMI), the last group's outflow
+    // goes to slab_out (the next GPU's slab_in, mapped here by IPC).  Both use
+    // slab_epoch, agreed by all ranks; null = an ordinary pair edge.
+    Granule* slab_in;
+    Granule* slab_out;
+    unsigned slab_epoch;
 };
 
 // Grid organisations (sw_kernels.hip):

@@ -178,15 +178,15 @@ __device__ __forceinline__ int code_of(unsigned raw, int k0, int lane, int C, in
 // Publish the right-edge outflow collected in lanes [64-C, 64) of a chunk that
 // started at step k0: rows k0 - (64W-1) .. k0 + C - 1 - (64W-1).
 template <int W, int C>
-__device__ __forceinline__ void publish_granules(const KParams& kp, const __amdgpu_buffer_rsrc_t out_rsrc, int k0,
+__device__ __forceinline__ void publish_granules(const unsigned epoch, const __amdgpu_buffer_rsrc_t out_rsrc, int k0,
                                                  int lane, int m, int IOH, int IOE) {
     const int row_out = k0 + (lane - (64 - C)) - (64 * W - 1);
     const bool st = lane >= 64 - C && row_out >= 0 && row_out < m;
     u32x4 g;
-    g.x = kp.epoch;
+    g.x = epoch;
     g.y = (unsigned)IOH;
     g.z = (unsigned)IOE;
-    g.w = granule_chk(kp.epoch, IOH, IOE, row_out);
+    g.w = granule_chk(epoch, IOH, IOE, row_out);
     __builtin_amdgcn_raw_buffer_store_b128(g, out_rsrc, st ? (unsigned)row_out * 16u : OOR, 0, AUX_SC1);
 }
 
@@ -218,13 +218,13 @@ __device__ void strip_pass(const KParams& kp, const PairDesc& pd, const int stri
         u32x4 g = g_nxt;
         // next chunk's rows in flight while this chunk computes
         raw_nxt = fetch_raw(row_rsrc, k0 + C, lane, C, m);
-        if (has_in) await_granules<C>(kp, in_rsrc, g, k0, lane, m, strip, failed);
+        if (has_in) await_granules<C>(kp, in_rsrc, g, k0, lane, m, strip, failed, kp.epoch);
         if (has_in) g_nxt = fetch_granules<C>(in_rsrc, k0 + C, lane, m);
         const int code = code_of<DNA>(raw, k0, lane, C, m);
         const bool real = has_in && k0 + lane < m;
         S.feed(lane, C, real ? (int)g.y : -go, real ? (int)g.z : -ge, code);
         S.template run<C>(l63, go, ge, ma, mi);
-        if (has_out) publish_granules<W, C>(kp, out_rsrc, k0, lane, m, S.IOH, S.IOE);
+        if (has_out) publish_granules<W, C>(kp.epoch, out_rsrc, k0, lane, m, S.IOH, S.IOE);
     }
     S.commit_max(kp, pd, lane);
 }
@@ -297,13 +297,17 @@ __global__ void __launch_bounds__(256) sw_chain_kernel(KParams kp) {
         const bool real = strip < pd.strips;
         Strip<W, DNA> S;
         S.setup(kp, pd, strip, lane);   // past-the-end strips are all dead columns
-        const bool gin = real && wave == 0 && strip > 0;
-        const bool gout = real && wave == 3 && strip < pd.strips - 1;
+        const int ngroups = (pd.strips + 3) / 4;
+        const bool last = strip == pd.strips - 1;
+        // the pair's first strip takes a slab inflow, its last strip feeds a slab outflow
+        const bool gin = real && wave == 0 && (strip > 0 || kp.slab_in != nullptr);
+        const bool gout = real && ((wave == 3 && !last) || (last && kp.slab_out != nullptr));
         const bool lin = real && wave > 0;
         const bool lout = real && wave < 3 && strip + 1 < pd.strips;
         // granule buffers exist only between groups: boundary g joins group g and g+1
-        const __amdgpu_buffer_rsrc_t in_rsrc = bnd_rsrc(kp, pd, group - 1);
-        const __amdgpu_buffer_rsrc_t out_rsrc = bnd_rsrc(kp, pd, group);
+        const __amdgpu_buffer_rsrc_t in_rsrc = group_rsrc(kp, pd, group - 1, ngroups);
+        const __amdgpu_buffer_rsrc_t out_rsrc = group_rsrc(kp, pd, group, ngroups);
+        const unsigned ep_in = group_epoch(kp, group - 1, ngroups), ep_out = group_epoch(kp, group, ngroups);
         const __amdgpu_buffer_rsrc_t row_rsrc =
             __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned char*>(kp.seq + pd.row_off), 0, m, RSRC_FLAGS);
         const int nloc = (m + SW - 1 + C - 1) / C;
@@ -332,7 +336,7 @@ __global__ void __launch_bounds__(256) sw_chain_kernel(KParams kp) {
                 const bool active = cc >= 0 && cc < nloc;
                 // consume the buffers before refilling them, so each refill can
                 // land in the registers the loop carries (no back-edge copies)
-                if constexpr (GIN) await_granules<C>(kp, in_rsrc, gbuf, k0, lane, m, strip, failed);
+                if constexpr (GIN) await_granules<C>(kp, in_rsrc, gbuf, k0, lane, m, strip, failed, ep_in);
                 const int code = code_of<DNA>(rbuf, k0, lane, C, m);
                 int hg_in = -go, eh_in = -ge;
                 const int row = k0 + lane;
@@ -349,7 +353,7 @@ __global__ void __launch_bounds__(256) sw_chain_kernel(KParams kp) {
                 S.feed(lane, C, hg_in, eh_in, code);
                 S.template run<C>(l63, go, ge, ma, mi);
                 if constexpr (GOUT) {
-                    publish_granules<W, C>(kp, out_rsrc, k0, lane, m, S.IOH, S.IOE);
+                    publish_granules<W, C>(ep_out, out_rsrc, k0, lane, m, S.IOH, S.IOE);
                 } else if (active && lout) {
                     const int row_out = k0 + (lane - (64 - C)) - (SW - 1);
                     if (lane >= 64 - C && row_out >= 0 && row_out < m) ring[wave][row_out & (R - 1)] = make_int2(S.IOH, S.IOE);
@@ -365,7 +369,8 @@ __global__ void __launch_bounds__(256) sw_chain_kernel(KParams kp) {
         };
         using T_ = std::true_type;
         using F_ = std::false_type;
-        if (gin) chunk_loop(T_{}, F_{});
+        if (gin && gout) chunk_loop(T_{}, T_{});   // a one-strip group between two slab edges
+        else if (gin) chunk_loop(T_{}, F_{});
         else if (gout) chunk_loop(F_{}, T_{});
         else chunk_loop(F_{}, F_{});
         if (real) S.commit_max(kp, pd, lane);
@@ -467,10 +472,14 @@ __global__ void __launch_bounds__(256) sw_flow_kernel(KParams kp) {
         if (strip >= pd.strips) continue;
         Strip<W, true> S;
         S.setup(kp, pd, strip, lane);
-        const int in_kind = wave > 0 ? FLOW_LDS : strip > 0 ? FLOW_GRANULE : FLOW_NONE;
-        const int out_kind = strip + 1 >= pd.strips ? FLOW_NONE : wave < 3 ? FLOW_LDS : FLOW_GRANULE;
-        const __amdgpu_buffer_rsrc_t in_rsrc = bnd_rsrc(kp, pd, group - 1);
-        const __amdgpu_buffer_rsrc_t out_rsrc = bnd_rsrc(kp, pd, group);
+        const int ngroups = (pd.strips + 3) / 4;
+        const int in_kind = wave > 0 ? FLOW_LDS : (strip > 0 || kp.slab_in != nullptr) ? FLOW_GRANULE : FLOW_NONE;
+        const int out_kind = strip + 1 >= pd.strips ? (kp.slab_out != nullptr ? FLOW_GRANULE : FLOW_NONE)
+                             : wave < 3           ? FLOW_LDS
+                                                  : FLOW_GRANULE;
+        const __amdgpu_buffer_rsrc_t in_rsrc = group_rsrc(kp, pd, group - 1, ngroups);
+        const __amdgpu_buffer_rsrc_t out_rsrc = group_rsrc(kp, pd, group, ngroups);
+        const unsigned ep_in = group_epoch(kp, group - 1, ngroups), ep_out = group_epoch(kp, group, ngroups);
         const int nloc = (m + SW - 1 + C - 1) / C;
         bool failed = false;
         const long long t_start = (long long)__builtin_amdgcn_s_memrealtime();
@@ -506,7 +515,7 @@ __global__ void __launch_bounds__(256) sw_flow_kernel(KParams kp) {
 #endif
                 int hg_in = -go, eh_in = -ge;
                 if constexpr (IN == FLOW_GRANULE) {
-                    await_granules<C>(kp, in_rsrc, gbuf, k0, lane, m, strip, failed);
+                    await_granules<C>(kp, in_rsrc, gbuf, k0, lane, m, strip, failed, ep_in);
                     const bool live = row < m;
                     hg_in = live ? (int)gbuf.y : -go;
                     eh_in = live ? (int)gbuf.z : -ge;
@@ -550,7 +559,7 @@ __global__ void __launch_bounds__(256) sw_flow_kernel(KParams kp) {
                 S.template run<C>(l63, go, ge, ma, mi);
                 const unsigned long long ts2 = SW_STAMP();
                 if constexpr (OUT == FLOW_GRANULE) {
-                    publish_granules<W, C>(kp, out_rsrc, k0, lane, m, S.IOH, S.IOE);
+                    publish_granules<W, C>(ep_out, out_rsrc, k0, lane, m, S.IOH, S.IOE);
                 } else if constexpr (OUT == FLOW_LDS) {
                     const int hi = k0 + C - SW;   // last row this chunk completes
                     if (hi >= 0) {
@@ -598,9 +607,11 @@ __global__ void __launch_bounds__(256) sw_flow_kernel(KParams kp) {
             else flow_loop(I2{}, I0{});
         } else if (in_kind == FLOW_GRANULE) {
             if (out_kind == FLOW_LDS) flow_loop(I1{}, I2{});
+            else if (out_kind == FLOW_GRANULE) flow_loop(I1{}, I1{});   // one-strip group between slab edges
             else flow_loop(I1{}, I0{});
         } else {
             if (out_kind == FLOW_LDS) flow_loop(I0{}, I2{});
+            else if (out_kind == FLOW_GRANULE) flow_loop(I0{}, I1{});   // a one-strip first slab
             else flow_loop(I0{}, I0{});
         }
         if (kp.trace != nullptr && lane == 0) {
@@ -793,7 +804,7 @@ __device__ void strip_pass_duo(const KParams& kp, const DuoDesc& d, const int st
         u32x4 g = g_nxt;
         raw0_nxt = fetch_raw(r0, k0 + C, lane, C, d.m[0]);
         raw1_nxt = fetch_raw(r1, k0 + C, lane, C, d.m[1]);
-        if (has_in) await_granules<C>(kp, in_rsrc, g, k0, lane, m, strip, failed);
+        if (has_in) await_granules<C>(kp, in_rsrc, g, k0, lane, m, strip, failed, kp.epoch);
         if (has_in) g_nxt = fetch_granules<C>(in_rsrc, k0 + C, lane, m);
         const unsigned code = codes_duo(raw0, raw1, k0, lane, C, d);
         if (lane < C) {
@@ -803,7 +814,7 @@ __device__ void strip_pass_duo(const KParams& kp, const DuoDesc& d, const int st
             S.IOR = code;
         }
         S.template run<C>(l63, go2, ge2, ma2, gom2);
-        if (has_out) publish_granules<W, C>(kp, out_rsrc, k0, lane, m, (int)S.IOA, (int)S.IOE);
+        if (has_out) publish_granules<W, C>(kp.epoch, out_rsrc, k0, lane, m, (int)S.IOA, (int)S.IOE);
     }
     S.commit_max(kp, d, lane);
 }

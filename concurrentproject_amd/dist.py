@@ -1,12 +1,17 @@
-"""Multi-GPU batch scoring: one process per GPU, pairs sharded by contiguous
-blocks, per-pair int32 scores gathered to rank 0 over RCCL (torch.distributed
-backend "nccl" on ROCm; "gloo" for CPU tests).
+"""Multi-GPU scoring: one process per GPU (torch.distributed backend "nccl" =
+RCCL on ROCm; "gloo" for CPU tests).
+
+* Batches: pairs sharded by contiguous blocks, per-pair int32 scores gathered
+  to rank 0 over RCCL.  This is the north-star's "independent pairs shard
+  across the GPUs of a node, RCCL only for the final score gather": no
+  data-path collective, the only exchange is npairs int32 scores per step.
+* One long pair (ColumnSlabs): the columns are cut into one
+  slab per rank; slab edges travel GPU to GPU as tagged granules stored by the
+  producing kernel into the next rank's IPC-mapped buffer, and the score is an
+  all-reduce(MAX) of one int.
 
 The reference has no multi-GPU path (no NCCL/MPI call
-sites); this is the north-star's "independent pairs shard across the GPUs of a
-node, RCCL only for the final score gather".  There is no data-path collective:
-each rank generates (or receives) its own shard and scores it locally; the
-only exchange is npairs int32 scores per step.
+sites).
 """
 from __future__ import annotations
 
@@ -55,3 +60,75 @@ def score_sharded(npairs: int, score_shard: Callable[[int, int], Sequence[int]],
     local = torch.tensor(list(score_shard(lo, hi)), dtype=torch.int32, device=device)
     full = gather_scores(local, npairs, group)
     return None if full is None else full.cpu().tolist()
+
+
+# ---- one pair split into column slabs -------------------------------
+
+def slab_max(local: torch.Tensor, group=None) -> torch.Tensor:
+    """All-reduce(MAX) of the per-slab maxima: the pair's score, on every rank (RCCL;
+    gloo reduces a host copy).  The only collective of the slab path."""
+    if local.is_cuda and dist.get_backend(group) == "gloo":
+        host = local.cpu()
+        dist.all_reduce(host, op=dist.ReduceOp.MAX, group=group)
+        local.copy_(host)
+        return local
+    dist.all_reduce(local, op=dist.ReduceOp.MAX, group=group)
+    return local
+
+
+class ColumnSlabs:
+    """One (seq1, seq2) pair split into column slabs, one per rank.
+
+    Rank r scores columns [bounds[r], bounds[r+1]) of seq1 against all m rows of
+    seq2 (lib: sw_score_slab_device).  The left edge of its slab -- H - G_INIT,
+    E - G_EXT of the previous slab's last column, one tagged 16-byte granule per
+    row -- is written straight into a buffer rank r owns by rank r-1's kernel,
+    through an IPC mapping of that buffer (xGMI peer stores on a node): no host
+    staging and no collective on the data path.  The ranks run as one wavefront
+    pipeline; the only collective is slab_max, the all-reduce of one int.
+
+    The all-reduce also orders launches: rank r's launch k+1 is queued behind
+    it, so it cannot overwrite rank r+1's inflow before launch k there has read
+    it; each launch tags its granules with a fresh epoch, common to all ranks."""
+
+    def __init__(self, n: int, m: int, flags: int, group=None):
+        from . import ipc_open, slab_alloc, slab_bounds
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        self.n, self.m, self.flags = n, m, flags
+        self.bounds = slab_bounds(n, m, self.world, flags)
+        self.inflow = slab_alloc(m) if self.rank > 0 else None
+        handles = [None] * self.world
+        dist.all_gather_object(handles, self.inflow.handle if self.inflow else None, group=group)
+        self.outflow = ipc_open(handles[self.rank + 1]) if self.rank + 1 < self.world else 0
+        self.epoch = 0
+        self.score = torch.zeros(1, dtype=torch.int32, device="cuda")
+        dist.barrier(group=group)   # every rank has mapped its outflow before any kernel runs
+
+    @property
+    def columns(self) -> tuple:
+        return self.bounds[self.rank], self.bounds[self.rank + 1]
+
+    def run(self, d_arena_ptr: int, col_off: int, row_off: int, stream: Optional[int] = None) -> torch.Tensor:
+        """Score this rank's slab of the pair whose columns start at byte col_off and
+        rows at row_off of the device arena; returns the pair's score (1-int tensor,
+        identical on every rank).  Asynchronous on `stream` (torch's current stream)."""
+        from . import score_slab_device
+        self.epoch += 1
+        lo, hi = self.columns
+        score_slab_device(d_arena_ptr, col_off + lo, hi - lo, row_off, self.m,
+                          self.inflow.ptr if self.inflow else 0, self.outflow, self.epoch,
+                          self.score.data_ptr(), self.flags, stream)
+        return slab_max(self.score, self.group)
+
+    def close(self) -> None:
+        from . import ipc_close
+        torch.cuda.synchronize()
+        dist.barrier(group=self.group)   # no kernel still writes a buffer that is about to go
+        if self.outflow:
+            ipc_close(self.outflow)
+            self.outflow = 0
+        if self.inflow is not None:
+            self.inflow.free()
+            self.inflow = None

@@ -83,6 +83,37 @@ int sw_score_batch_device(const unsigned char* d_arena,
                           int npairs, int* d_scores, int flags, void* stream);
 int sw_stream_status(void* stream);
 
+/* ---- one pair split into column slabs across GPUs (no reference counterpart;
+ * the C5 pair N = 2^20 over the GPUs of a node) ---------
+ * Rank r of R scores columns [bounds[r], bounds[r+1]) of seq1 against all of
+ * seq2.  Its left edge (H - G_INIT, E - G_EXT of the previous slab's last
+ * column, one 16-byte tagged granule per row) is written straight into rank
+ * r's inflow buffer by rank r-1's kernel, through an IPC mapping of that
+ * buffer (xGMI stores, no host staging); the pair's score is the max of the
+ * R slab maxima (an all-reduce(MAX) of one int).  dist.ColumnSlabs drives it.
+ *
+ * sw_slab_bounds: R+1 column bounds; every slab but the last is a multiple of
+ *   the kernel's column quantum (returned, > 0; 63 or 64*W).  flags must say
+ *   SW_FLAG_DNA or SW_FLAG_BYTES (all ranks must plan the same kernel).
+ * sw_score_slab_device: one slab, sequences resident in device memory:
+ *   columns d_arena[col_off, col_off+n), rows d_arena[row_off, row_off+m).
+ *   d_inflow / d_outflow: granule buffers of m rows (NULL = the matrix border
+ *   / the pair's last column); epoch != 0, the same on every rank and fresh
+ *   for every launch over the same buffers.  *d_score = this slab's max H.
+ *   Asynchronous on `stream` as sw_score_batch_device.
+ * sw_slab_alloc: a zeroed inflow buffer of m granules; returns 1 (fine-grained
+ *   memory) or 2 (device memory), -1 on error; ipc_handle (SW_IPC_HANDLE_BYTES,
+ *   may be NULL) receives its hipIpcMemHandle_t for the writing rank.
+ * sw_ipc_open / sw_ipc_close: map / unmap another process's buffer. */
+#define SW_IPC_HANDLE_BYTES 64
+int sw_slab_bounds(long long n, int m, int nslabs, int flags, long long* bounds);
+int sw_score_slab_device(const unsigned char* d_arena, int64_t col_off, int n, int64_t row_off, int m,
+                         void* d_inflow, void* d_outflow, unsigned epoch, int* d_score, int flags, void* stream);
+int sw_slab_alloc(int m, void** d_buf, void* ipc_handle);
+int sw_slab_free(void* d_buf);
+int sw_ipc_open(const void* ipc_handle, void** d_ptr);
+int sw_ipc_close(void* d_ptr);
+
 /* Tuning knobs (process-wide).  Keys:
  *   "W"        columns per lane: 0 = auto, 1, 2, 4, 8
  *   "C"        rows per strip hand-off chunk: 0 = auto, 16, 32, 64

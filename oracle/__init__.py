@@ -74,6 +74,9 @@ def lib():
                                 ctypes.POINTER(u8p), ctypes.POINTER(ctypes.c_int), ctypes.c_int,
                                 pp, ctypes.POINTER(ctypes.c_int), ctypes.c_int, ctypes.c_int]
         L.swo_batch.restype = ctypes.c_int
+        ip = ctypes.POINTER(ctypes.c_int)
+        L.swo_slab.argtypes = [u8p, u8p, ctypes.c_int, ctypes.c_int, pp, ip, ip, ip, ip]
+        L.swo_slab.restype = ctypes.c_int
         L.swo_gen_pair.argtypes = [ctypes.c_uint64, ctypes.c_int, u8p, u8p]
         L.swo_mt64_size.restype = ctypes.c_size_t
         L.swo_mt64_seed.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
@@ -112,6 +115,35 @@ def score_linear(seq1, seq2, params: Params = DEFAULT, rows: int | None = None) 
     p = params.c()
     r = len(b) if rows is None else rows
     return lib().swo_linear_rows(pa, pb, len(a), len(b), ctypes.byref(p), r)
+
+
+def slab(cols, seq2, params: Params = DEFAULT, edge=None) -> tuple:
+    """One column slab (swo_slab): ``cols`` are the slab's columns, ``edge`` the
+    (H, E) int32 arrays of the column left of it (None: the matrix border).
+    Returns (max H over the slab, (H, E) of its last column)."""
+    a, pa = _u8(cols); b, pb = _u8(seq2)
+    m = len(b)
+    ip = ctypes.POINTER(ctypes.c_int)
+    out_h = np.zeros(m, dtype=np.int32); out_e = np.zeros(m, dtype=np.int32)
+    if edge is None:
+        in_h = in_e = None
+    else:
+        eh, ee = (np.ascontiguousarray(x, dtype=np.int32) for x in edge)
+        in_h, in_e = eh.ctypes.data_as(ip), ee.ctypes.data_as(ip)
+    p = params.c()
+    best = lib().swo_slab(pa, pb, len(a), m, ctypes.byref(p), in_h, in_e,
+                          out_h.ctypes.data_as(ip), out_e.ctypes.data_as(ip))
+    if best < 0:
+        raise RuntimeError("swo_slab failed")
+    return best, (out_h, out_e)
+
+
+def score_slab(seq1, seq2, lo: int, hi: int, params: Params = DEFAULT) -> tuple:
+    """Columns [lo, hi) of seq1 as a slab, with the true left edge (columns [0, lo)
+    computed first).  Returns (max H over the slab, its last column's (H, E))."""
+    a = as_u8(seq1)
+    edge = None if lo == 0 else slab(a[:lo], seq2, params)[1]
+    return slab(a[lo:hi], seq2, params, edge)
 
 
 def score_wavefront(seq1, seq2, params: Params = DEFAULT, threads: int = 8) -> int:

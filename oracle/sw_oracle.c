@@ -21,6 +21,8 @@
  *   swo_linear    lazySmith.cpp:15-42 (row state H_prev/H_curr/E/F; the lazy-F
  *                                    fix-up loop :43-62 never changes H, see
  *                                    DESIGN.md, so it is omitted)
+ *   swo_slab      lazySmith.cpp:15-42 over one column slab with a left edge
+ *                                    (the multi-GPU column-slab checker)
  *   swo_wavefront multi-threaded linear-space restatement (column blocks
  *                                    pipelined over row blocks); same cell
  *                                    recurrence as swo_linear, used to make
@@ -123,6 +125,43 @@ int swo_linear_rows(const unsigned char* seq1, const unsigned char* seq2, int n,
 int swo_linear(const unsigned char* seq1, const unsigned char* seq2, int n, int m,
                const swo_params* p) {
     return swo_linear_rows(seq1, seq2, n, m, p, m);
+}
+
+/*
+ * One column slab of the same linear-space recurrence (lazySmith.cpp:15-42
+ * with a left edge): columns seq1[0..n) of a pair whose column just left of
+ * the slab ended row i with H = in_h[i-1], E = in_e[i-1] (NULL: the matrix
+ * border, 0, main.cpp:43-52).  Writes the slab's last column to out_h / out_e
+ * (if non-NULL) and returns the max H over the slab's cells.  Chaining slabs
+ * left to right reproduces swo_linear exactly (the checker of the multi-GPU
+ * column-slab path).
+ */
+int swo_slab(const unsigned char* seq1, const unsigned char* seq2, int n, int m, const swo_params* p,
+             const int* in_h, const int* in_e, int* out_h, int* out_e) {
+    if (n <= 0 || m <= 0) return 0;
+    int* Hp = (int*)calloc((size_t)n + 1, sizeof(int));
+    int* Hc = (int*)calloc((size_t)n + 1, sizeof(int));
+    int* F = (int*)calloc((size_t)n + 1, sizeof(int));
+    if (!Hp || !Hc || !F) { free(Hp); free(Hc); free(F); return -1; }
+    int best = 0;
+    for (int i = 1; i <= m; ++i) {
+        const unsigned char di = seq2[i - 1];
+        int e = in_e ? in_e[i - 1] : 0;    /* E[i][left] */
+        Hc[0] = in_h ? in_h[i - 1] : 0;    /* H[i][left]; Hp[0] holds H[i-1][left] */
+        for (int j = 1; j <= n; ++j) {
+            e = imax(e - p->gap_ext, Hc[j - 1] - p->gap_init);
+            F[j] = imax(F[j] - p->gap_ext, Hp[j] - p->gap_init);
+            int h = Hp[j - 1] + swo_s(p, seq1[j - 1], di);
+            h = imax(h, e); h = imax(h, F[j]); h = imax(h, 0);
+            Hc[j] = h;
+            best = imax(best, h);
+        }
+        if (out_h) out_h[i - 1] = Hc[n];
+        if (out_e) out_e[i - 1] = e;
+        int* t = Hp; Hp = Hc; Hc = t;
+    }
+    free(Hp); free(Hc); free(F);
+    return best;
 }
 
 /* ---------------------------------------------------------------------------

@@ -65,6 +65,25 @@ def test_options_host_side():
     sw.set_option("W", 0); sw.set_option("C", 0); sw.set_option("timeout", 30)
 
 
+def test_slab_bounds_host_side():
+    """Column-slab planning (host only): flow2 slabs are multiples of its 63-column
+    stride, the chain / flow kernels' of 64*W; the alphabet must be stated."""
+    import concurrentproject_amd as sw
+    sw.set_params(sw.Params())
+    b = sw.slab_bounds(65536, 65536, 4, sw.SW_FLAG_DNA)          # rows fit in LDS: flow2
+    assert b[0] == 0 and b[-1] == 65536 and all(x % 63 == 0 for x in b[1:-1]) and b == sorted(b)
+    b = sw.slab_bounds(1 << 20, 1 << 20, 8, sw.SW_FLAG_DNA)      # C5: rows too long for LDS -> chain
+    assert b[-1] == 1 << 20 and all(x % 64 == 0 for x in b[1:-1]) and len(set(b)) == 9
+    assert max(y - x for x, y in zip(b, b[1:])) - min(y - x for x, y in zip(b, b[1:])) < 8 * 64
+    b = sw.slab_bounds(10000, 3000, 3, sw.SW_FLAG_BYTES)
+    assert all(x % 64 == 0 for x in b[1:-1]) and b[-1] == 10000
+    assert sw.slab_bounds(500, 500, 1, sw.SW_FLAG_DNA) == [0, 500]
+    with pytest.raises(sw.SwError):
+        sw.slab_bounds(100, 100, 4, sw.SW_FLAG_DNA)             # narrower than 4 quanta
+    with pytest.raises(sw.SwError):
+        sw.slab_bounds(10000, 100, 2, 0)                        # alphabet not stated
+
+
 def test_product_generator_matches_oracle(oracle_mod, golden):
     """The library's synthetic generator (bench inputs) == the pinned oracle generator."""
     import concurrentproject_amd as sw

@@ -71,6 +71,69 @@ def test_sharded_gather(world, npairs):
     assert all(r[3] is None for r in res[1:])
 
 
+def _slab_worker(rank, world, port, n, m, q):
+    """One rank of the column-slab decomposition on CPU: the slab bounds the GPU
+    path uses (sw.slab_bounds), the oracle standing in for the slab kernel, the
+    left edge received from rank-1 and the right edge sent to rank+1 (gloo
+    point-to-point in place of the kernels' IPC stores), and the score reduced
+    with the product's slab_max."""
+    import sys
+    sys.path.insert(0, ROOT)
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import oracle
+        import concurrentproject_amd as sw
+        from concurrentproject_amd.dist import slab_max
+        a, b = oracle.gen_pair(4242, n)
+        b = b[:m]
+        bounds = sw.slab_bounds(n, m, world, sw.SW_FLAG_DNA)
+        lo, hi = bounds[rank], bounds[rank + 1]
+        edge = None
+        if rank > 0:
+            eh = torch.empty(m, dtype=torch.int32)
+            ee = torch.empty(m, dtype=torch.int32)
+            dist.recv(eh, src=rank - 1)
+            dist.recv(ee, src=rank - 1)
+            edge = (eh.numpy(), ee.numpy())
+        best, (oh, oe) = oracle.slab(a[lo:hi], b, edge=edge)
+        if rank + 1 < world:
+            dist.send(torch.from_numpy(np.ascontiguousarray(oh)), dst=rank + 1)
+            dist.send(torch.from_numpy(np.ascontiguousarray(oe)), dst=rank + 1)
+        score = slab_max(torch.tensor([best], dtype=torch.int32))
+        q.put((rank, int(score.item()), bounds, None))
+    except Exception as e:
+        q.put((rank, None, None, repr(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n,m", [(2, 700, 300), (3, 1000, 450)])
+def test_column_slabs_gloo(world, n, m):
+    """The one-pair multi-GPU decomposition is exact: slabs chained through their
+    edges, max-reduced, give the whole pair's score on every rank."""
+    import oracle
+    a, b = oracle.gen_pair(4242, n)
+    exp = oracle.score_linear(a, b[:m])
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_slab_worker, args=(r, world, port, n, m, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=300) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, got, bounds, err in res:
+        assert err is None, (rank, err)
+        assert got == exp, (rank, got, exp, bounds)
+    assert len(set(res[0][2])) == world + 1   # every rank got a non-empty slab
+
+
 def test_c3_prefix_matches_fixture():
     """The gathered order is the fixture order: shard r holds pairs seeded 8192 + k, k in [lo, hi)."""
     from concurrentproject_amd.dist import shard_bounds

@@ -63,6 +63,25 @@ def test_wavefront_equals_linear(oracle_mod):
             assert oracle_mod.score_wavefront(a, b, p, threads=4) == oracle_mod.score_linear(a, b, p)
 
 
+def test_slabs_chain_to_linear(oracle_mod):
+    """Column slabs chained through their (H, E) edges reproduce the whole pair:
+    the max over slabs is score_linear, for any cut points (the multi-GPU slab
+    checker itself, pinned to the lazySmith restatement)."""
+    rng = np.random.default_rng(8)
+    for p in (oracle_mod.Params(), oracle_mod.Params(2, -3, 5, 2), oracle_mod.Params(1, -1, 3, 1)):
+        for _ in range(5):
+            n, m = int(rng.integers(2, 900)), int(rng.integers(1, 600))
+            a = np.frombuffer(b"ACGT", np.uint8)[rng.integers(0, 4, n)]
+            b = np.frombuffer(b"ACGT", np.uint8)[rng.integers(0, 4, m)]
+            cuts = sorted(set([0, n] + [int(x) for x in rng.integers(1, n, 3)]))
+            best, edge = 0, None
+            for lo, hi in zip(cuts, cuts[1:]):
+                s, edge = oracle_mod.slab(a[lo:hi], b, p, edge)
+                assert s == oracle_mod.score_slab(a, b, lo, hi, p)[0]
+                best = max(best, s)
+            assert best == oracle_mod.score_linear(a, b, p), (p, n, m, cuts)
+
+
 def test_restatement_vs_reference_build(oracle_mod):
     """Only where oracle/_ref exists (build container): the reference's own code."""
     if oracle_mod.ref_lib() is None:
