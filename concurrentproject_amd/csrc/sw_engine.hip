@@ -451,7 +451,11 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
     if (duo) std::memcpy(c->hduo.p, job.duos.data(), np * sizeof(DuoDesc));
     else std::memcpy(c->hdesc.p, job.pairs.data(), np * sizeof(PairDesc));
     std::memcpy(c->hibase.p, job.item_base.data(), (np + 1) * sizeof(int));
+    const Ctrl* ctrl_before = c->ctrl.p;
     if (c->desc.ensure(np, s) || c->duo.ensure(np, s) || c->ibase.ensure(np + 1, s) || c->ctrl.ensure(1, s)) return -1;
+    // a fresh control block holds whatever the allocator recycled: clear the sticky
+    // error fields once (afterwards only check_ctrl resets them, after reporting)
+    if (c->ctrl.p != ctrl_before) HIPCHK(hipMemsetAsync(c->ctrl.p, 0, sizeof(Ctrl), s));
     if (job.bnd_granules) {
         size_t freeb = 0, totb = 0;
         HIPCHK(hipMemGetInfo(&freeb, &totb));
