@@ -40,7 +40,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", default="auto", choices=["auto", "pair", "batch"])
+    ap.add_argument("--workload", default="auto", choices=["auto", "pair", "batch", "slab"])
+    ap.add_argument("--slab-of", type=int, default=0,
+                    help="slab workload, one GPU: time slab 0 of a K-way column split alone (per-rank cost)")
     ap.add_argument("--n", type=int, default=0, help="override sequence length")
     ap.add_argument("--pairs-per-gpu", type=int, default=1024)
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU baseline leg")
@@ -78,6 +80,22 @@ def cpu_baseline(kind: str, n: int, budget_s: float, params):
         return {"value": cells / t_tot / 1e9, "unit": "GCUPS", "cores": 1, "kind": "port",
                 "sample": "main.cpp SmithWatermanScore restated (full (m+1)x(n+1)x3 int32 matrices), "
                           "1 thread, on row prefixes of the C2 pair up to %d x %d; %.1f s" % (rows, len(a), t_tot)}
+    if kind == "slab":
+        # C5: main.cpp's full matrices would need 13.2 TB; lazySmith.cpp's linear-space
+        # restatement on row prefixes of the C5 pair
+        a, b = oracle.gen_pair(1048576 if n == 1 << 20 else n, n)
+        rows, spent, cells, t_tot = 4, 0.0, 0, 0.0
+        while True:
+            t0 = time.perf_counter()
+            oracle.score_linear(a, b, p, rows=rows)
+            dt = time.perf_counter() - t0
+            cells += rows * len(a); t_tot += dt; spent += dt
+            if spent > budget_s or rows >= len(b):
+                break
+            rows = min(len(b), rows * 2)
+        return {"value": cells / t_tot / 1e9, "unit": "GCUPS", "cores": 1, "kind": "port",
+                "sample": "lazySmith.cpp LazySmith restated (linear space; main.cpp's matrices need 13.2 TB), "
+                          "1 thread, on row prefixes of the C5 pair up to %d x %d; %.1f s" % (rows, len(a), t_tot)}
     # batch: one pair per thread (embarrassingly parallel), a bounded subset of pairs
     threads = max(1, min(16, os.cpu_count() or 1))
     npairs = threads
@@ -126,6 +144,21 @@ def main():
                            "C2-size pairs N=%d, one per GPU (seeds 65536+rank)" % N,
                "N": N, "pairs_per_gpu": 1, "global_pairs": world,
                "parallelism": "pair-sharded x%d + RCCL gather of scores" % world if world > 1 else "single GPU"}
+    elif workload == "slab":
+        # C5: ONE pair N = 2^20 (seed 1048576); with --gpus N its columns are cut into
+        # one slab per rank (dist.ColumnSlabs: slab edges stored GPU to GPU through
+        # IPC-mapped buffers, all-reduce(MAX) of the score).  Every rank holds the
+        # whole pair (2 MB).  One GPU: the plain single-pair path, or with --slab-of K
+        # slab 0 of a K-way split alone (edge into a local buffer): the per-rank cost.
+        N = args.n or (1 << 20)
+        a, b = sw.gen_pair(1048576 if N == 1 << 20 else N, N)
+        host = np.concatenate([a, b])
+        offs_a, offs_b, lens = [0], [N], [N]
+        npairs_rank = 1
+        cfg = {"workload": "C5 single pair N=%d (seed 1048576)" % N, "N": N, "pairs_per_gpu": 1.0 / world,
+               "global_pairs": 1,
+               "parallelism": ("column slabs x%d, GPU-to-GPU edge stores + RCCL all-reduce(MAX)" % world
+                               if world > 1 else "single GPU")}
     else:
         from concurrentproject_amd.dist import shard_bounds
         N = args.n or 8192
@@ -153,15 +186,51 @@ def main():
         from concurrentproject_amd.dist import gather_scores
         return gather_scores(scores, total_pairs)     # RCCL gather of the per-pair int32 scores
 
-    def step():
+    # the launch of one step (the timed kernel), then the step's collective
+    slabs, slab_buf, slab_cols = None, None, None
+    cells_rank = sum(int(x) * int(y) for x, y in zip(lens, lens))
+    cells_job = cells_rank * world
+    if workload == "slab" and dist is not None:
+        from concurrentproject_amd.dist import ColumnSlabs
+        slabs = ColumnSlabs(N, N, sw.SW_FLAG_DNA)
+        lo, hi = slabs.columns
+        cells_rank, cells_job = (hi - lo) * N, N * N
+        cfg["slab_columns"] = [lo, hi]
+    elif workload == "slab" and args.slab_of > 1:
+        bounds = sw.slab_bounds(N, N, args.slab_of, sw.SW_FLAG_DNA)
+        slab_cols, slab_buf = bounds[1], sw.slab_alloc(N)
+        cells_rank = cells_job = slab_cols * N
+        cfg.update(workload="C5 slab 0 of a %d-way column split, alone (per-rank cost)" % args.slab_of,
+                   slab_columns=[0, slab_cols])
+    epoch = [0]
+
+    def launch():
+        if slabs is not None:
+            epoch[0] += 1
+            lo, hi = slabs.columns
+            sw.score_slab_device(arena.data_ptr(), lo, hi - lo, N, N, slabs.inflow.ptr if slabs.inflow else 0,
+                                 slabs.outflow, slabs.epoch + epoch[0], scores.data_ptr(), sw.SW_FLAG_DNA, sptr)
+        elif slab_buf is not None:
+            epoch[0] += 1
+            sw.score_slab_device(arena.data_ptr(), 0, slab_cols, N, N, 0, slab_buf.ptr, epoch[0],
+                                 scores.data_ptr(), sw.SW_FLAG_DNA, sptr)
+        else:
+            sw.score_batch_device(arena.data_ptr(), offs_a, lens, offs_b, lens, scores.data_ptr(),
+                                  flags=1, stream=sptr)
+
+    def collective():
         nonlocal gathered
-        sw.score_batch_device(arena.data_ptr(), offs_a, lens, offs_b, lens, scores.data_ptr(),
-                              flags=1, stream=sptr)
-        if dist is not None:
+        if dist is None:
+            return
+        if slabs is not None:
+            from concurrentproject_amd.dist import slab_max
+            slab_max(scores)                           # RCCL all-reduce(MAX) of one int
+        else:
             gathered = gather()
 
     for _ in range(args.warmup):
-        step()
+        launch()
+        collective()
     sw.stream_status(sptr)
     torch.cuda.synchronize()
 
@@ -173,11 +242,9 @@ def main():
     t0 = time.perf_counter()
     for i in range(args.steps):
         starts[i].record(stream)
-        sw.score_batch_device(arena.data_ptr(), offs_a, lens, offs_b, lens, scores.data_ptr(),
-                              flags=1, stream=sptr)
+        launch()
         ends[i].record(stream)
-        if dist is not None:
-            gathered = gather()
+        collective()
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
@@ -193,9 +260,12 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         t_max = float(tt.item())
 
-    cells_rank = sum(int(x) * int(y) for x, y in zip(lens, lens))
-    total_cells = cells_rank * world * args.steps
+    total_cells = cells_job * args.steps
     value = total_cells / t_max / 1e9
+    if slabs is not None:
+        slabs.close()
+    if slab_buf is not None:
+        slab_buf.free()
 
     # PCIe-inclusive rate of the synchronous host entry point (H2D of the two
     # sequences + launch + score D2H): reported beside `value`, never as it
@@ -220,6 +290,11 @@ def main():
             ref = gold.get("C4", gold.get("C3", {})).get("scores", [])
             if len(ref) >= len(allsc):
                 parity = "ok" if allsc == ref[:len(allsc)] else "MISMATCH"
+        elif workload == "slab" and N == 1 << 20 and slab_buf is None:
+            # C5 has no CPU golden (~2 h single-core): the property-checked score
+            # (default plan == transposed == W=4 plan, tools/c5_check.py)
+            parity = ("ok (vs property-checked 119470, CPU-unpinned)" if scores[0].item() == 119470
+                      else "MISMATCH")
 
     if rank == 0:
         per_launch_cells = cells_rank
