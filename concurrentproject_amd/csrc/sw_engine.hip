@@ -56,7 +56,7 @@ std::mutex g_param_mu;
 Params g_params;
 
 std::atomic<long long> g_opt_W{0}, g_opt_C{0}, g_opt_bytes{0}, g_opt_timeout{30}, g_opt_blocks{0}, g_opt_orient{0},
-    g_opt_mode{-1}, g_opt_trace{0};
+    g_opt_mode{-1}, g_opt_trace{0}, g_opt_duo_f16{1};
 
 // orientation: 0 = engine policy, 1 = seq1 across lanes (columns), 2 = seq2 across lanes
 bool want_swap(bool single, long long len1, long long len2) {
@@ -181,6 +181,7 @@ struct Job {
     int mode = MODE_STRIP;
     bool dna = true;
     std::vector<DuoDesc> duos;   // MODE_DUO only
+    bool duo_f16 = false;        // MODE_DUO: max3 through v_pk_maximum3_f16 (duo_f16_fits)
 };
 
 bool is_dna_byte(unsigned char c) { return c == 'A' || c == 'C' || c == 'G' || c == 'T'; }
@@ -263,6 +264,16 @@ bool duo_fits(const Job& job, const Params& p) {
     if (!job.dna || p.gap_init + p.match > 65535 || p.gap_ext > 65535 || p.match - p.mismatch > 254) return false;
     for (auto& d : job.pairs)
         if ((long long)std::max(p.match, 1) * std::min(d.n, d.m) + p.match > 65535) return false;
+    return true;
+}
+
+// The duo kernel's f16-max3 variant reads u16 values as f16 bit patterns, exact
+// below 0x7C00 (no Inf/NaN encodings): every t, E, F, H and running max is at
+// most max H + MATCH <= MATCH*(min(n,m)+1).
+bool duo_f16_fits(const Job& job, const Params& p) {
+    if (!g_opt_duo_f16.load()) return false;
+    for (auto& d : job.pairs)
+        if ((long long)std::max(p.match, 1) * (std::min(d.n, d.m) + 1) > 0x7BFF) return false;
     return true;
 }
 
@@ -355,6 +366,7 @@ int finalize_mode(Job& job, const Params& prm) {
     if (forced_duo || (g_opt_mode.load() < 0 && job.mode == MODE_PAIRWG)) {
         if (duo_fits(job, prm)) {
             job.mode = MODE_DUO;
+            job.duo_f16 = duo_f16_fits(job, prm);
             plan_duos(job);
             return 0;
         }
@@ -477,6 +489,7 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
     int max_m = 0;
     for (const PairDesc& d : job.pairs) max_m = std::max(max_m, d.m);
     LaunchCfg cfg{job.W, job.C, job.dna, 0, job.mode, max_m};
+    cfg.duo_f16 = job.mode == MODE_DUO && job.duo_f16;
     const int wpc = waves_per_cu(c, cfg);
     const int items = job.item_base[np];
     long long blocks = g_opt_blocks.load();
@@ -976,6 +989,8 @@ int sw_set_option(const char* key, long long v) {
     } else if (k == "mode") {
         if (v < -1 || v > 5) return -1;
         g_opt_mode = v;
+    } else if (k == "duo16") {   // 1 = duo max3 through v_pk_maximum3_f16 when exact (default), 0 = u16 max only
+        g_opt_duo_f16 = v ? 1 : 0;
     } else {
         set_err("unknown option '%s'", key);
         return -1;
@@ -994,6 +1009,7 @@ long long sw_get_option(const char* key) {
     if (k == "orient") return g_opt_orient;
     if (k == "trace") return g_opt_trace;
     if (k == "mode") return g_opt_mode;
+    if (k == "duo16") return g_opt_duo_f16;
     return -1;
 }
 

@@ -108,6 +108,7 @@ struct LaunchCfg {
     int blocks;     // persistent workgroups (256 threads = 4 waves)
     int mode;       // MODE_*
     int max_m;      // longest row sequence (MODE_FLOW stages it in LDS)
+    bool duo_f16 = false;   // MODE_DUO: max3 through v_pk_maximum3_f16 (every value < 0x7C00)
 };
 
 // MODE_FLOW stages a pair's row codes in LDS: one byte per row plus the

@@ -654,6 +654,18 @@ __device__ __forceinline__ u16x2 vmax2(u16x2 a, u16x2 b) { return __builtin_elem
 __device__ __forceinline__ u16x2 vsubs2(u16x2 a, u16x2 b) { return __builtin_elementwise_sub_sat(a, b); }
 __device__ __forceinline__ u16x2 splat2(int v) { return u16x2{(unsigned short)v, (unsigned short)v}; }
 
+// v_pk_maximum3_f16 as an UNSIGNED 16-bit max3 (gfx950): for halves in [0, 0x7BFF]
+// -- sign clear, no Inf/NaN encodings, f16 denormals preserved (the HIP default
+// mode) -- the IEEE maximum of the f16 values is the integer maximum of the bit
+// patterns (checked exhaustively on the GPU: tools/check_pkmax3.hip).  One VOP3P
+// instead of two v_pk_max_u16; the host enables it only when every score, E, F
+// and t fits below 0x7C00 (duo_f16_fits).
+__device__ __forceinline__ u16x2 vmax3h(u16x2 a, u16x2 b, u16x2 c) {
+    unsigned d;
+    asm("v_pk_maximum3_f16 %0, %1, %2, %3" : "=v"(d) : "v"(as32(a)), "v"(as32(b)), "v"(as32(c)));
+    return as16(d);
+}
+
 constexpr unsigned SENT_DUO = 0x0C0D0C0Du;   // selector 13 in both halves -> penalty 0xFF
 
 __device__ __forceinline__ DuoDesc load_duo(const KParams& kp, int idx) {
@@ -674,7 +686,7 @@ __device__ __forceinline__ DuoDesc load_duo(const KParams& kp, int idx) {
     return d;
 }
 
-template <int W>
+template <int W, bool M3>
 struct StripDuo {
     unsigned pA[W], pB[W];                   // column penalty words: pair 0 (perm src1), pair 1 (perm src0)
     u16x2 aA[W], aB[W];                      // A = H + MATCH, ping-pong (diagonal source)
@@ -717,6 +729,7 @@ struct StripDuo {
         const u16x2 ehL0 = as16((unsigned)dpp_shr1((int)IOE, (int)as32(eh[W - 1])));
         const unsigned rL0 = (unsigned)dpp_shr1((int)IOR, (int)r[W - 1]);
         const u16x2 hgL0 = vsubs2(aL0, gom2);   // H - G_INIT of the left neighbour, from its A
+        u16x2 tOdd = splat2(0);                 // M3: t of position p+1, folded with p's into M
 #pragma unroll
         for (int p = W - 1; p >= 0; --p) {
             const int q = p > 0 ? p - 1 : 0;
@@ -728,8 +741,16 @@ struct StripDuo {
             const u16x2 t = vsubs2(aD, pen);                 // max(H_diag + s, 0)
             const u16x2 E = vmax2(ehL, hgL);
             const u16x2 F = vmax2(fh[p], hg[p]);
-            const u16x2 H = vmax2(vmax2(t, E), F);
-            M = vmax2(M, t);
+            u16x2 H;
+            if constexpr (M3) {
+                H = vmax3h(t, E, F);
+                if constexpr (W == 1) M = vmax2(M, t);
+                else if (p & 1) tOdd = t;                    // positions (2k+1, 2k): one max3 into M
+                else M = vmax3h(M, tOdd, t);
+            } else {
+                H = vmax2(vmax2(t, E), F);
+                M = vmax2(M, t);
+            }
             aCur[p] = H + ma2;
             hg[p] = vsubs2(H, go2);
             eh[p] = vsubs2(E, ge2);
@@ -775,14 +796,14 @@ __device__ __forceinline__ unsigned codes_duo(unsigned raw0, unsigned raw1, int 
     return 0x0C000C00u | (s1 << 16) | s0;
 }
 
-template <int W, int C>
+template <int W, int C, bool M3>
 __device__ void strip_pass_duo(const KParams& kp, const DuoDesc& d, const int strip, const int lane) {
     constexpr int SW = 64 * W;
     const int m = d.m_pad;
     const bool l63 = lane == 63;
     const u16x2 go2 = splat2(kp.gap_init), ge2 = splat2(kp.gap_ext), ma2 = splat2(kp.match),
                 gom2 = splat2(kp.gap_init + kp.match);
-    StripDuo<W> S;
+    StripDuo<W, M3> S;
     S.setup(kp, d, strip, lane);
     const bool has_in = strip > 0;
     const bool has_out = strip < d.strips - 1;
@@ -821,13 +842,15 @@ __device__ void strip_pass_duo(const KParams& kp, const DuoDesc& d, const int st
 
 // Kernel 4 (DNA batches, 16-bit scores): workgroup b scores duos b, b+gridDim,
 // ...; wave w runs strips w, w+4, ... of each duo (as sw_pairwg_kernel).
-template <int W, int C>
+// M3: H = max3 and the running max fold two positions per v_pk_maximum3_f16
+// (scores below 0x7C00 only, LaunchCfg::duo_f16).
+template <int W, int C, bool M3>
 __global__ void __launch_bounds__(256) sw_duo_kernel(KParams kp) {
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     for (int di = blockIdx.x; di < kp.npairs; di += gridDim.x) {
         const DuoDesc d = load_duo(kp, di);
-        for (int strip = wave; strip < d.strips; strip += 4) strip_pass_duo<W, C>(kp, d, strip, lane);
+        for (int strip = wave; strip < d.strips; strip += 4) strip_pass_duo<W, C, M3>(kp, d, strip, lane);
     }
 }
 
@@ -860,7 +883,11 @@ hipError_t launch_t(const LaunchCfg& cfg, const KParams& kp, hipStream_t s) {
             }
             return hipErrorInvalidValue;
         case MODE_DUO:
-            if constexpr (DNA) { hipLaunchKernelGGL((sw_duo_kernel<W, C>), dim3(cfg.blocks), dim3(256), 0, s, kp); break; }
+            if constexpr (DNA) {
+                if (cfg.duo_f16) hipLaunchKernelGGL((sw_duo_kernel<W, C, true>), dim3(cfg.blocks), dim3(256), 0, s, kp);
+                else hipLaunchKernelGGL((sw_duo_kernel<W, C, false>), dim3(cfg.blocks), dim3(256), 0, s, kp);
+                break;
+            }
             return hipErrorInvalidValue;
         default: return hipErrorInvalidValue;
     }
@@ -877,7 +904,7 @@ int waves_t(int mode) {
             if constexpr (DNA) return occupancy_waves(sw_flow_kernel<W, C>);
             return 0;
         case MODE_DUO:
-            if constexpr (DNA) return occupancy_waves(sw_duo_kernel<W, C>);
+            if constexpr (DNA) return occupancy_waves(sw_duo_kernel<W, C, true>);
             return 4;
         default: return 4;
     }

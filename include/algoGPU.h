@@ -125,6 +125,8 @@ int sw_ipc_close(void* d_ptr);
  *              2 = lock-step strip groups (single long pairs),
  *              3 = packed 16-bit pair duos (DNA batches with scores < 65535),
  *              4 = free-running strip groups, rows staged in LDS (long DNA pairs)
+ *   "duo16"    1 = (default) packed duos take max3 through v_pk_maximum3_f16 when every
+ *              value stays below 0x7C00 (MATCH*(min(n,m)+1) <= 31743), 0 = u16 max only
  * Returns 0, or -1 for an unknown key / bad value. */
 int sw_set_option(const char* key, long long value);
 long long sw_get_option(const char* key);

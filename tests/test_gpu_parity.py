@@ -301,6 +301,35 @@ def test_duo_batches(engine, oracle_mod):
             assert engine.score_batch(pairs, prm) == exp, (prm, npairs)
 
 
+def test_duo_f16_max3_boundary(engine, oracle_mod):
+    """The duo's v_pk_maximum3_f16 variant (u16 halves read as f16 bit patterns) is
+    used while MATCH*(min(n,m)+1) <= 0x7BFF; identical pairs put the running max,
+    H and t right at that edge, one base more takes the u16-max duo.  Both agree
+    with the oracle, and the variant agrees with duo16=0 on random batches."""
+    rng = np.random.default_rng(21)
+    s = _rand_dna(rng, 31743)
+    engine.set_option("mode", 3)
+    try:
+        assert engine.score_batch([(s[:31742], s[:31742]), (s[:9000], s[:9000])]) == [31742, 9000]
+        assert engine.score_batch([(s, s), (s[:10], s[:10])]) == [31743, 10]
+        pairs = []
+        for _ in range(9):
+            n, m = int(rng.integers(300, 3000)), int(rng.integers(300, 3000))
+            a = _rand_dna(rng, n)
+            b = np.resize(a, m).copy()
+            mut = rng.random(m) < 0.15
+            b[mut] = _rand_dna(rng, int(mut.sum()))
+            pairs.append((a, b))
+        for prm in (engine.Params(), engine.Params(3, -2, 7, 1)):
+            exp = [oracle_mod.score_linear(a, b, oracle_mod.Params(*prm.__dict__.values())) for a, b in pairs]
+            for flag in (1, 0):
+                engine.set_option("duo16", flag)
+                assert engine.score_batch(pairs, prm) == exp, (prm, flag)
+    finally:
+        engine.set_option("duo16", 1)
+        engine.set_option("mode", -1)
+
+
 def test_duo_16bit_boundary(engine):
     """H + MATCH must fit 16 bits: 65534 identical bases is the largest exact duo case;
     one more forces the int32 kernels (auto) or an error (forced duo)."""
