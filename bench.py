@@ -49,6 +49,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--W", type=int, default=0)
     ap.add_argument("--C", type=int, default=0)
+    ap.add_argument("--mode", type=int, default=-1, help="engine option 'mode' (-1 = automatic plan)")
     ap.add_argument("--params", default="1,-1,1,1", help="MATCH,MISMATCH,G_INIT,G_EXT")
     return ap.parse_args()
 
@@ -126,6 +127,8 @@ def main():
         sw.set_option("W", args.W)
     if args.C:
         sw.set_option("C", args.C)
+    if args.mode >= 0:
+        sw.set_option("mode", args.mode)
 
     workload = args.workload
     if workload == "auto":

@@ -49,7 +49,7 @@ class _Stats(ctypes.Structure):
     _fields_ = [("kernel_ms", ctypes.c_float), ("total_ms", ctypes.c_float), ("cells", ctypes.c_longlong),
                 ("W", ctypes.c_int), ("C", ctypes.c_int), ("dna", ctypes.c_int), ("blocks", ctypes.c_int),
                 ("waves_per_cu", ctypes.c_int), ("items", ctypes.c_int), ("boundary_bytes", ctypes.c_longlong),
-                ("mode", ctypes.c_int)]
+                ("mode", ctypes.c_int), ("variant", ctypes.c_int)]
 
 
 _lib = None

@@ -56,7 +56,7 @@ std::mutex g_param_mu;
 Params g_params;
 
 std::atomic<long long> g_opt_W{0}, g_opt_C{0}, g_opt_bytes{0}, g_opt_timeout{30}, g_opt_blocks{0}, g_opt_orient{0},
-    g_opt_mode{-1}, g_opt_trace{0}, g_opt_duo_f16{1};
+    g_opt_mode{-1}, g_opt_trace{0}, g_opt_duo_f16{1}, g_opt_f2stream{0};
 
 // orientation: 0 = engine policy, 1 = seq1 across lanes (columns), 2 = seq2 across lanes
 bool want_swap(bool single, long long len1, long long len2) {
@@ -182,6 +182,7 @@ struct Job {
     bool dna = true;
     std::vector<DuoDesc> duos;   // MODE_DUO only
     bool duo_f16 = false;        // MODE_DUO: max3 through v_pk_maximum3_f16 (duo_f16_fits)
+    bool f2_stream = false;      // MODE_FLOW2: row codes streamed (rows too long to stage in LDS)
 };
 
 bool is_dna_byte(unsigned char c) { return c == 'A' || c == 'C' || c == 'G' || c == 'T'; }
@@ -315,9 +316,14 @@ void plan_duos(Job& job) {
 // the packed duo kernel when it is exact, or honour a forced duo request.
 // MODE_FLOW2 (sw_flow2.hip): W = 1, DNA, every score byte s + G_INIT a signed
 // byte above the -128 sentinel, and the row codes fit in LDS.
-bool flow2_fits(const Job& job, const Params& p, int max_m) {
+// Rows that fit in LDS are staged once per workgroup; longer ones (C5) stream
+// through per-wave code rings (sw_flow2.hip, STREAM), as do all with "f2stream" = 1.
+bool flow2_fits(const Job& job, const Params& p) {
     return job.dna && job.W == 1 && flow2_variant_exists(job.C) && p.match + p.gap_init <= 127 &&
-           p.mismatch + p.gap_init >= -127 && flow2_stage_bytes(max_m, job.C) <= flow2_stage_max(job.C);
+           p.mismatch + p.gap_init >= -127;
+}
+bool flow2_staged(const Job& job, int max_m) {
+    return g_opt_f2stream.load() == 0 && flow2_stage_bytes(max_m, job.C) <= flow2_stage_max(job.C);
 }
 
 // Re-plan a grouped job for MODE_FLOW2: strips of 64 columns overlapping by one.
@@ -337,13 +343,23 @@ void plan_flow2(Job& job) {
 int finalize_mode(Job& job, const Params& prm) {
     int max_m = 0;
     for (const PairDesc& d : job.pairs) max_m = std::max(max_m, d.m);
+    // a single pair too wide for W = 1 under the 2048-strip rule: flow2 still runs it
+    // fastest at W = 1 (its 10.7-VALU step, rows streamed when they exceed the LDS;
+    // C5: 545 ms vs 894 ms for the W = 8 chain)
+    if (g_opt_mode.load() < 0 && g_opt_W.load() == 0 && job.mode == MODE_CHAIN && job.W > 1 &&
+        job.pairs.size() == 1) {
+        Job w1 = job;
+        plan(w1, 1, pick_C(1), true, MODE_CHAIN);
+        if (flow2_fits(w1, prm)) job = w1;
+    }
     if (job.mode == MODE_FLOW2 || (g_opt_mode.load() < 0 && job.mode == MODE_CHAIN)) {
-        if (flow2_fits(job, prm, max_m)) {
+        if (flow2_fits(job, prm)) {
             plan_flow2(job);
+            job.f2_stream = !flow2_staged(job, max_m);
             return 0;
         }
         if (job.mode == MODE_FLOW2) {
-            set_err("flow2 mode needs W=1, C in {16,32,64}, {A,C,G,T} rows that fit in LDS and "
+            set_err("flow2 mode needs W=1, C in {16,32,64}, {A,C,G,T} sequences and "
                     "-127 <= MISMATCH+G_INIT, MATCH+G_INIT <= 127");
             return -1;
         }
@@ -490,6 +506,7 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
     for (const PairDesc& d : job.pairs) max_m = std::max(max_m, d.m);
     LaunchCfg cfg{job.W, job.C, job.dna, 0, job.mode, max_m};
     cfg.duo_f16 = job.mode == MODE_DUO && job.duo_f16;
+    cfg.f2_stream = job.mode == MODE_FLOW2 && job.f2_stream;
     const int wpc = waves_per_cu(c, cfg);
     const int items = job.item_base[np];
     long long blocks = g_opt_blocks.load();
@@ -553,6 +570,7 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
     t_stats.waves_per_cu = wpc;
     t_stats.items = items;
     t_stats.mode = job.mode;
+    t_stats.variant = (cfg.duo_f16 ? 1 : 0) | (cfg.f2_stream ? 2 : 0);
     t_stats.boundary_bytes = (long long)(job.bnd_granules * sizeof(Granule));
     c->last = s;
     return 0;
@@ -991,6 +1009,8 @@ int sw_set_option(const char* key, long long v) {
         g_opt_mode = v;
     } else if (k == "duo16") {   // 1 = duo max3 through v_pk_maximum3_f16 when exact (default), 0 = u16 max only
         g_opt_duo_f16 = v ? 1 : 0;
+    } else if (k == "f2stream") {   // 1 = flow2 streams row codes even when they fit in LDS (tests)
+        g_opt_f2stream = v ? 1 : 0;
     } else {
         set_err("unknown option '%s'", key);
         return -1;
@@ -1010,6 +1030,7 @@ long long sw_get_option(const char* key) {
     if (k == "trace") return g_opt_trace;
     if (k == "mode") return g_opt_mode;
     if (k == "duo16") return g_opt_duo_f16;
+    if (k == "f2stream") return g_opt_f2stream;
     return -1;
 }
 

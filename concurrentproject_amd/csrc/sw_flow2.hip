@@ -90,11 +90,24 @@ __device__ __forceinline__ int sbyte(unsigned w) {
     else return (int)(signed char)(w >> (8 * B));
 }
 
-template <int C>
+// STREAM (rows too long to stage, e.g. C5's 2^20): instead of the pair's staged
+// codes, each wave keeps its own ring of F2_CR row codes in LDS -- row r in slot
+// (r + 64) mod F2_CR, slots [0, C) mirrored behind the ring so that a lane's
+// unaligned 4-row read never wraps -- and refills it one chunk ahead: C lanes load
+// the raw bytes of chunk c+4 (buffer_load_ubyte, two chunks of latency cover) and
+// store the codes of chunk c+2 (two ds_write_b8).  The step loop is unchanged.
+constexpr int F2_CR = 256;
+
+template <int C, bool STREAM>
 __global__ void __launch_bounds__(256) sw_flow2_kernel(KParams kp) {
     static_assert(C % 4 == 0 && 64 % C == 0 && 2 * C + 64 <= F2_R, "chunk");
+    // STREAM ring: during chunk c the reads span rows [k0 + C - 63, k0 + 2C) and the
+    // writes rows [k0 + 2C, k0 + 3C): no slot is rewritten while still read
+    static_assert(!STREAM || 3 * C + 63 <= F2_CR, "code ring");
     constexpr int R = F2_R;
-    extern __shared__ unsigned char rc[];    // rc[row + 64]: 4..7 = A,C,G,T; 0 = no row
+    constexpr int CRB = F2_CR + C + 64;      // STREAM ring + mirror + per-lane sinks, bytes per wave
+    extern __shared__ unsigned char rc[];    // rc[row + 64]: 4..7 = A,C,G,T; 0 = no row (staged mode)
+    __shared__ __attribute__((aligned(16))) unsigned char cring[STREAM ? 4 : 1][STREAM ? CRB : 16];
     __shared__ int2 ring[4][R];              // ring w: outflow rows of wave w (row r in slot r mod R)
     __shared__ int2 sink[4][64];             // lanes that publish nothing write here
     __shared__ int prod[4], cons[4], psink[4][64];
@@ -115,9 +128,9 @@ __global__ void __launch_bounds__(256) sw_flow2_kernel(KParams kp) {
         const int nloc = (m + 64 + C - 1) / C;   // lane 63's last row is out at step m + 63
         if (tid < 4) { prod[tid] = 0; cons[tid] = 0; }
         for (int i = tid; i < 4 * R; i += 256) ring[i / R][i % R] = make_int2(-go, -ge);
-        {
-            const __amdgpu_buffer_rsrc_t row_rsrc =
-                __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned char*>(kp.seq + pd.row_off), 0, m, RSRC_FLAGS);
+        const __amdgpu_buffer_rsrc_t row_rsrc =
+            __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned char*>(kp.seq + pd.row_off), 0, m, RSRC_FLAGS);
+        if constexpr (!STREAM) {
             const int nst = flow2_stage_bytes(m, C);
             for (int i = tid * 4; i < nst; i += 1024) {
                 unsigned w = 0;
@@ -165,6 +178,35 @@ __global__ void __launch_bounds__(256) sw_flow2_kernel(KParams kp) {
         int2* const out_ring = ring[wave];
         // per-lane code address: lane l reads rows k - l .. k - l + 3 (unaligned dword)
         const unsigned char* const code_base = rc + 64 - lane;
+        // STREAM: this wave's code ring; codes of chunk cc's rows from their raw bytes
+        unsigned char* const cr = cring[STREAM ? wave : 0];
+        auto raw_of = [&](const int cc) __attribute__((always_inline)) {
+            const int row = cc * C + lane;
+            return __builtin_amdgcn_raw_buffer_load_b8(row_rsrc, lane < C && row < m ? (unsigned)row : OOR, 0, 0);
+        };
+        auto put_codes = [&](const unsigned raw, const int cc) __attribute__((always_inline)) {
+            const int row = cc * C + lane;
+            const bool wl = lane < C;
+            const unsigned char code = (unsigned char)(wl && row < m ? 4u + (unsigned)dna_code(raw) : 0u);
+            const int s1 = wl ? ((row + 64) & (F2_CR - 1)) : F2_CR + C + lane;
+            const int s2 = wl && s1 < C ? F2_CR + s1 : F2_CR + C + lane;
+            cr[s1] = code;
+            cr[s2] = code;
+        };
+        // where lane l's reads of chunk k0's rows start (STREAM: in the ring)
+        auto code_at = [&](const int k0) __attribute__((always_inline)) -> const unsigned char* {
+            if constexpr (STREAM) return cr + ((k0 + 64 - lane) & (F2_CR - 1));
+            else return code_base + k0;
+        };
+        unsigned rq0 = 0, rq1 = 0;   // STREAM: raw bytes of chunks c+2, c+3 in flight
+        if constexpr (STREAM) {
+            for (int i = lane; i < CRB / 4; i += 64) reinterpret_cast<unsigned*>(cr)[i] = 0u;   // rows < 0: no row
+            const unsigned r0 = raw_of(0), r1 = raw_of(1);
+            put_codes(r0, 0);
+            put_codes(r1, 1);
+            rq0 = raw_of(2);
+            rq1 = raw_of(3);
+        }
 
         auto flow_loop = [&](auto in_c, auto out_c) __attribute__((always_inline)) {
             constexpr int IN = decltype(in_c)::value, OUT = decltype(out_c)::value;
@@ -175,7 +217,7 @@ __global__ void __launch_bounds__(256) sw_flow2_kernel(KParams kp) {
                 gq[i] = IN == FLOW_GRANULE ? fetch_granules<C>(in_rsrc, i * C, lane, m) : u32x4{0u, 0u, 0u, 0u};
             unsigned D[C / 4];
 #pragma unroll
-            for (int u = 0; u < C / 4; ++u) D[u] = load_u32_unaligned(code_base + 4 * u);
+            for (int u = 0; u < C / 4; ++u) D[u] = load_u32_unaligned(code_at(0) + 4 * u);
             int cons_seen = 0;
             int spec_avail = -1;                 // progress word read with spec_v (-1: none)
             int2 spec_v = make_int2(0, 0);
@@ -306,8 +348,13 @@ __global__ void __launch_bounds__(256) sw_flow2_kernel(KParams kp) {
 #ifdef SW_TIMELINE
                 if (c == 0) t_first = realtime_waited();
 #endif
+                if constexpr (STREAM) {   // refill the ring: codes of chunk c+2, raw bytes of chunk c+4
+                    put_codes(rq0, c + 2);
+                    rq0 = rq1;
+                    rq1 = raw_of(c + 4);
+                }
 #pragma unroll
-                for (int u = 0; u < C / 4; ++u) D[u] = load_u32_unaligned(code_base + k0 + C + 4 * u);
+                for (int u = 0; u < C / 4; ++u) D[u] = load_u32_unaligned(code_at(k0 + C) + 4 * u);
                 // ---- C anti-diagonal steps
 #pragma unroll
                 for (int j = 0; j < C; j += 4) {
@@ -389,28 +436,31 @@ __global__ void __launch_bounds__(256) sw_flow2_kernel(KParams kp) {
     }
 }
 
-template <int C>
+template <int C, bool STREAM>
 hipError_t launch_c(const LaunchCfg& cfg, const KParams& kp, hipStream_t s) {
     // at least half the CU's LDS: one workgroup per CU, so no strip ever shares a
     // SIMD with another (a co-resident waiting workgroup's polls steal issue slots
-    // from a strip on the critical path)
-    const int dyn = std::max(flow2_stage_bytes(cfg.max_m, C), LDS_PER_CU / 2 + 1024 - flow2_static_lds(C));
-    if (dyn > flow2_stage_max(C)) return hipErrorInvalidValue;
+    // from a strip on the critical path); STREAM stages nothing, the rest is padding
+    const int pad = LDS_PER_CU / 2 + 1024 - flow2_static_lds(C);
+    const int dyn = STREAM ? pad : std::max(flow2_stage_bytes(cfg.max_m, C), pad);
+    const int lim = flow2_stage_max(C) - (STREAM ? 4 * (F2_CR + C + 64) : 0);
+    if (dyn > lim) return hipErrorInvalidValue;
     static int dyn_set = 0;   // raise the dynamic-LDS limit once per variant
     if (dyn > 64 * 1024 && dyn_set == 0) {
-        const hipError_t e = hipFuncSetAttribute((const void*)sw_flow2_kernel<C>,
-                                                 hipFuncAttributeMaxDynamicSharedMemorySize, flow2_stage_max(C));
+        const hipError_t e = hipFuncSetAttribute((const void*)sw_flow2_kernel<C, STREAM>,
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, lim);
         if (e != hipSuccess) return e;
         dyn_set = 1;
     }
-    hipLaunchKernelGGL((sw_flow2_kernel<C>), dim3(cfg.blocks), dim3(256), (size_t)dyn, s, kp);
+    hipLaunchKernelGGL((sw_flow2_kernel<C, STREAM>), dim3(cfg.blocks), dim3(256), (size_t)dyn, s, kp);
     return hipGetLastError();
 }
 
 template <int C>
 int waves_c() {
     int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)sw_flow2_kernel<C>, 256, 0) != hipSuccess) return 4;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)sw_flow2_kernel<C, false>, 256, 0) != hipSuccess)
+        return 4;
     return nb * 4;
 }
 
@@ -420,9 +470,9 @@ bool flow2_variant_exists(int C) { return C == 16 || C == 32 || C == 64; }
 
 hipError_t launch_sw_flow2(const LaunchCfg& cfg, const KParams& kp, hipStream_t stream) {
     switch (cfg.C) {
-        case 16: return launch_c<16>(cfg, kp, stream);
-        case 32: return launch_c<32>(cfg, kp, stream);
-        case 64: return launch_c<64>(cfg, kp, stream);
+        case 16: return cfg.f2_stream ? launch_c<16, true>(cfg, kp, stream) : launch_c<16, false>(cfg, kp, stream);
+        case 32: return cfg.f2_stream ? launch_c<32, true>(cfg, kp, stream) : launch_c<32, false>(cfg, kp, stream);
+        case 64: return cfg.f2_stream ? launch_c<64, true>(cfg, kp, stream) : launch_c<64, false>(cfg, kp, stream);
         default: return hipErrorInvalidValue;
     }
 }

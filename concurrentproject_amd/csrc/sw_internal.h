@@ -109,6 +109,7 @@ struct LaunchCfg {
     int mode;       // MODE_*
     int max_m;      // longest row sequence (MODE_FLOW stages it in LDS)
     bool duo_f16 = false;   // MODE_DUO: max3 through v_pk_maximum3_f16 (every value < 0x7C00)
+    bool f2_stream = false; // MODE_FLOW2: row codes streamed through per-wave LDS rings (rows too long to stage)
 };
 
 // MODE_FLOW stages a pair's row codes in LDS: one byte per row plus the

@@ -139,6 +139,7 @@ typedef struct {
     int W, C, dna, blocks, waves_per_cu, items;
     long long boundary_bytes;
     int mode;
+    int variant;            /* bit 0: duo max3 via v_pk_maximum3_f16; bit 1: flow2 streams row codes */
 } sw_stats;
 int sw_last_stats(sw_stats* out);
 

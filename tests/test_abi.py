@@ -72,9 +72,15 @@ def test_slab_bounds_host_side():
     sw.set_params(sw.Params())
     b = sw.slab_bounds(65536, 65536, 4, sw.SW_FLAG_DNA)          # rows fit in LDS: flow2
     assert b[0] == 0 and b[-1] == 65536 and all(x % 63 == 0 for x in b[1:-1]) and b == sorted(b)
-    b = sw.slab_bounds(1 << 20, 1 << 20, 8, sw.SW_FLAG_DNA)      # C5: rows too long for LDS -> chain
-    assert b[-1] == 1 << 20 and all(x % 64 == 0 for x in b[1:-1]) and len(set(b)) == 9
-    assert max(y - x for x, y in zip(b, b[1:])) - min(y - x for x, y in zip(b, b[1:])) < 8 * 64
+    b = sw.slab_bounds(1 << 20, 1 << 20, 8, sw.SW_FLAG_DNA)      # C5: flow2 streaming its row codes
+    assert b[-1] == 1 << 20 and all(x % 63 == 0 for x in b[1:-1]) and len(set(b)) == 9
+    assert max(y - x for x, y in zip(b, b[1:])) - min(y - x for x, y in zip(b, b[1:])) < 8 * 63
+    sw.set_option("mode", 2)                                     # forced chain: 64*W columns
+    try:
+        b = sw.slab_bounds(1 << 20, 1 << 20, 8, sw.SW_FLAG_DNA)
+        assert all(x % 64 == 0 for x in b[1:-1])
+    finally:
+        sw.set_option("mode", -1)
     b = sw.slab_bounds(10000, 3000, 3, sw.SW_FLAG_BYTES)
     assert all(x % 64 == 0 for x in b[1:-1]) and b[-1] == 10000
     assert sw.slab_bounds(500, 500, 1, sw.SW_FLAG_DNA) == [0, 500]

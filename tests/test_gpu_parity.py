@@ -219,6 +219,59 @@ def test_flow2_ragged(engine, oracle_mod):
         engine.set_option("orient", 0)
 
 
+def test_flow2_streamed_rows(engine, oracle_mod):
+    """flow2 with the row codes streamed through per-wave LDS rings (rows too long
+    to stage, the C5 path): forced on the ragged flow2 shapes and chosen
+    automatically for a pair whose 200000 rows exceed the LDS."""
+    rng = np.random.default_rng(78)
+    shapes = [(1, 1), (1, 300), (300, 1), (63, 63), (64, 64), (65, 65), (127, 126), (128, 300), (253, 252),
+              (255, 1000), (256, 17), (1000, 64), (2017, 2100), (4096, 4000)]
+    pairs = []
+    for n, m in shapes:
+        a = _rand_dna(rng, n)
+        b = _rand_dna(rng, m)
+        if rng.random() < 0.5 and m > 10:
+            b = np.resize(a, m).copy()
+            mut = rng.random(m) < 0.05
+            b[mut] = _rand_dna(rng, int(mut.sum()))
+        pairs.append((a, b))
+    engine.set_option("orient", 1)
+    engine.set_option("f2stream", 1)
+    try:
+        for prm in (engine.Params(), engine.Params(2, -3, 5, 2), engine.Params(60, -120, 67, 9)):
+            op = oracle_mod.Params(prm.match, prm.mismatch, prm.gap_init, prm.gap_ext)
+            exp = [oracle_mod.score_linear(a, b, op) for a, b in pairs]
+            engine.set_option("mode", 5)
+            for C in (16, 32, 64):
+                engine.set_option("C", C)
+                assert [engine.score(a, b, prm) for a, b in pairs] == exp, (C, prm)
+                assert engine.last_stats()["variant"] & 2
+                assert engine.score_batch(pairs, prm) == exp, (C, prm)
+            engine.set_option("C", 0)
+            engine.set_option("mode", -1)
+        engine.set_option("f2stream", 0)
+        # long rows: automatic flow2 (W = 1 for 700 columns) with streamed codes
+        a = _rand_dna(rng, 700)
+        b = _similar_rows(rng, a, 200000)
+        e = oracle_mod.score_linear(a, b)
+        assert engine.score(a, b) == e
+        st = engine.last_stats()
+        assert st["mode"] == 5 and st["variant"] & 2, st
+    finally:
+        engine.set_option("f2stream", 0)
+        engine.set_option("mode", -1)
+        engine.set_option("C", 0)
+        engine.set_option("orient", 0)
+
+
+def _similar_rows(rng, a, m):
+    """m rows that repeat `a` with 5% point mutations (long local alignments)."""
+    b = np.resize(a, m).copy()
+    mut = rng.random(m) < 0.05
+    b[mut] = _rand_dna(rng, int(mut.sum()))
+    return b
+
+
 def test_edges(engine, oracle_mod):
     assert engine.SmithWatermanScoreCUDA(b"", b"ACGT") == 0
     assert engine.SmithWatermanScoreCUDA(b"ACGT", b"") == 0
