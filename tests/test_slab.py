@@ -38,7 +38,7 @@ def _defaults(engine):
     engine.set_option("mode", -1)
     yield
     engine.set_params(engine.Params())
-    for k in ("W", "C", "bytes", "blocks", "orient"):
+    for k in ("W", "C", "bytes", "blocks", "orient", "f2stream"):
         engine.set_option(k, 0)
     engine.set_option("mode", -1)
 
@@ -124,6 +124,7 @@ def test_slabs_threads_every_kernel(engine, oracle_mod, nslabs):
     engine.set_option("blocks", 48)          # every slab's grid co-resides on the one GPU
     cases = [
         ("flow2", engine.Params(), engine.SW_FLAG_DNA, -1, 5),
+        ("flow2-stream", engine.Params(2, -3, 5, 2), engine.SW_FLAG_DNA, -1, 5),   # codes streamed (C5 path)
         ("flow", engine.Params(2, -3, 130, 2), engine.SW_FLAG_DNA, -1, 4),
         ("chain", engine.Params(2, -3, 5, 2), engine.SW_FLAG_DNA, 2, 2),
         ("bytes", engine.Params(1, -1, 3, 1), engine.SW_FLAG_BYTES, -1, 2),
@@ -131,6 +132,7 @@ def test_slabs_threads_every_kernel(engine, oracle_mod, nslabs):
     for name, prm, flags, mode, want_mode in cases:
         engine.set_params(prm)
         engine.set_option("mode", mode)
+        engine.set_option("f2stream", 1 if name == "flow2-stream" else 0)
         op = oracle_mod.Params(prm.match, prm.mismatch, prm.gap_init, prm.gap_ext)
         for n, m in ((nslabs * 600 + 77, 1500), (nslabs * 1300, 901)):
             a = _rand_dna(rng, n)
@@ -142,6 +144,7 @@ def test_slabs_threads_every_kernel(engine, oracle_mod, nslabs):
             got, bounds, stats = _run_threads(engine, a, b, nslabs, flags)
             assert max(got) == exp, (name, n, m, got, exp, bounds)
             assert all(s["mode"] == want_mode for s in stats), (name, [s["mode"] for s in stats])
+            assert all(bool(s["variant"] & 2) == (name == "flow2-stream") for s in stats), name
             # a slab reports max(0, max t) over its cells (t = diagonal + s): an H that
             # comes from a gap opened in an earlier slab is counted there, so a slab's
             # value is at most the oracle's max H over its columns, and the pair's
@@ -189,7 +192,7 @@ def _free_port():
     return p
 
 
-def _ipc_worker(rank, world, port, n, m, seed, q):
+def _ipc_worker(rank, world, port, n, m, seed, stream_codes, q):
     import sys
     sys.path.insert(0, ROOT)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -202,6 +205,7 @@ def _ipc_worker(rank, world, port, n, m, seed, q):
         from concurrentproject_amd.dist import ColumnSlabs
         sw.set_option("timeout", 10)
         sw.set_option("blocks", 64)          # both ranks' grids fit the one GPU together
+        sw.set_option("f2stream", stream_codes)
         a, b = sw.gen_pair(seed, n)
         b = b[:m]
         arena = torch.from_numpy(np.concatenate([a, b])).cuda()
@@ -219,9 +223,11 @@ def _ipc_worker(rank, world, port, n, m, seed, q):
         dist.destroy_process_group()
 
 
-def test_slabs_two_processes_ipc(oracle_mod):
+@pytest.mark.parametrize("stream_codes", [0, 1])
+def test_slabs_two_processes_ipc(oracle_mod, stream_codes):
     """Two ranks, one GPU: rank 0's kernel writes its right edge into rank 1's
-    inflow buffer through an IPC mapping, as between the GPUs of a node."""
+    inflow buffer through an IPC mapping, as between the GPUs of a node; flow2
+    with staged and with streamed row codes."""
     import torch.multiprocessing as mp
     n, m, seed = 8192, 3000, 8192
     a, b = oracle_mod.gen_pair(seed, n)
@@ -229,7 +235,7 @@ def test_slabs_two_processes_ipc(oracle_mod):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_ipc_worker, args=(r, 2, port, n, m, seed, q)) for r in range(2)]
+    procs = [ctx.Process(target=_ipc_worker, args=(r, 2, port, n, m, seed, stream_codes, q)) for r in range(2)]
     for p in procs:
         p.start()
     try:

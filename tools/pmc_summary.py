@@ -4,7 +4,7 @@ profile summaries.
 
     python tools/pmc_summary.py gpurun_out/prof r01
 
-For each workload (c2 -> pair, c3 -> batch):
+For each workload (c2 -> pair, c3 -> batch, c5 -> slab on one GPU):
   * copies the kernel-trace stats and the FETCH_SIZE / WRITE_SIZE counter CSVs
     and the bench line to profiles/<round>_<cfg>_*;
   * writes profiles/pmc_<workload>.json, which bench.py reads for
@@ -24,8 +24,8 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ALGO_BYTES_PER_CELL = 12
-CELLS = {"c2": 65536 * 65536, "c3": 1024 * 8192 * 8192}
-WORKLOAD = {"c2": "pair", "c3": "batch"}
+CELLS = {"c2": 65536 * 65536, "c3": 1024 * 8192 * 8192, "c5": (1 << 20) * (1 << 20)}
+WORKLOAD = {"c2": "pair", "c3": "batch", "c5": "slab"}
 
 
 def _rows(path):
@@ -48,7 +48,7 @@ def per_launch(path):
 def main():
     src, rnd = sys.argv[1], sys.argv[2]
     prof = os.path.join(ROOT, "profiles")
-    for cfg in ("c2", "c3"):
+    for cfg in ("c2", "c3", "c5"):
         stats = os.path.join(src, "kt_" + cfg, cfg + "_kernel_stats.csv")
         fetch = os.path.join(src, "fetch_" + cfg, cfg + "_counter_collection.csv")
         write = os.path.join(src, "write_" + cfg, cfg + "_counter_collection.csv")

@@ -1,11 +1,18 @@
 set -e
+# Round profiles: bench lines, rocprofv3 kernel-trace stats and FETCH_SIZE / WRITE_SIZE
+# passes (one counter set per run) for C2 (pair), C3 (batch) and C5 (slab workload, 1 GPU).
+# usage (on the GPU box): bash tools/prof_round.sh [c2 c3 c5]
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out/prof
-timeout -k 10 200 python bench.py --steps 10 --warmup 2 > gpurun_out/prof/bench_c2.json 2> gpurun_out/prof/bench_c2.err
-timeout -k 10 200 python bench.py --workload batch --steps 5 --warmup 1 --no-cpu-baseline > gpurun_out/prof/bench_c3.json 2> gpurun_out/prof/bench_c3.err
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof/kt_c2 -o c2 -- python bench.py --steps 5 --warmup 1 --no-cpu-baseline > gpurun_out/prof/kt_c2.log 2>&1
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof/kt_c3 -o c3 -- python bench.py --workload batch --steps 5 --warmup 1 --no-cpu-baseline > gpurun_out/prof/kt_c3.log 2>&1
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/prof/fetch_c2 -o c2 -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/prof/fetch_c2.log 2>&1
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/prof/write_c2 -o c2 -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/prof/write_c2.log 2>&1
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/prof/fetch_c3 -o c3 -- python bench.py --workload batch --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/prof/fetch_c3.log 2>&1
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/prof/write_c3 -o c3 -- python bench.py --workload batch --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/prof/write_c3.log 2>&1
+which="${*:-c2 c3 c5}"
+for w in $which; do
+  case $w in
+    c2) args="--steps 10 --warmup 2"; pargs="--steps 5 --warmup 1";;
+    c3) args="--workload batch --steps 5 --warmup 1"; pargs="--workload batch --steps 3 --warmup 1";;
+    c5) args="--workload slab --steps 3 --warmup 1 --cpu-seconds 10"; pargs="--workload slab --steps 2 --warmup 1";;
+  esac
+  timeout -k 10 240 python bench.py $args > gpurun_out/prof/bench_$w.json 2> gpurun_out/prof/bench_$w.err
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof/kt_$w -o $w -- python bench.py $pargs --no-cpu-baseline > gpurun_out/prof/kt_$w.log 2>&1
+  timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/prof/fetch_$w -o $w -- python bench.py $pargs --no-cpu-baseline > gpurun_out/prof/fetch_$w.log 2>&1
+  timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/prof/write_$w -o $w -- python bench.py $pargs --no-cpu-baseline > gpurun_out/prof/write_$w.log 2>&1
+done
