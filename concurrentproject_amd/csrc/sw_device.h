@@ -11,6 +11,7 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int DPP_WAVE_ROL1 = 0x134;
 constexpr int DPP_WAVE_SHR1 = 0x138;
+constexpr int DPP_WAVE_SHL1 = 0x130;
 constexpr unsigned RSRC_FLAGS = 0x00020000u;   // raw buffer, gfx950 (cdna_hip_programming.md T8)
 constexpr int AUX_SC1 = 16;                    // cache policy: sc1 (L1 bypass / write-through)
 constexpr unsigned OOR = 0xFFFFFFF0u;          // out-of-range buffer offset: load returns 0, store dropped

@@ -54,8 +54,6 @@ constexpr int F2_R = 256;   // ring rows per link (power of two, >= 2C + 64)
 #define SW_F2_HALFPUB 1     // workgroup-edge strips publish granules every half chunk
 #endif
 
-constexpr int DPP_WAVE_SHL1 = 0x130;
-
 // v_add_u32_dpp wave_shr:1 with the destination tied to 'old': lanes 1..63 get
 // src[l-1] + k, lane 0 (no source, bound_ctrl off) keeps old.  Inline asm because
 // no builtin ties a DPP-VOP2 destination to a live register.  The hazard a VALU

@@ -722,12 +722,18 @@ struct StripDuo {
         L0 = ma2; M = splat2(0); IOA = as32(ma2); IOE = 0u; IOR = SENT_DUO;
     }
 
-    __device__ __forceinline__ void step(u16x2 (&aCur)[W], const u16x2 (&aPrev)[W], const bool l63, const u16x2 go2,
+    // One anti-diagonal step; S = the step's index mod W.  Position p's row code lives
+    // in r[(p - S) mod W]: the slot of position p at step S is the slot of position
+    // p-1 at step S-1, so the codes advance one position per step with no register
+    // move, and the code entering position 0 (lane l-1's position W-1, or the inflow
+    // at lane 0) is written in place by the DPP that fetches it.
+    template <int S>
+    __device__ __forceinline__ void step(u16x2 (&aCur)[W], const u16x2 (&aPrev)[W], const u16x2 go2,
                                          const u16x2 ge2, const u16x2 ma2, const u16x2 gom2) {
-        const unsigned ioa = (unsigned)dpp_rol1((int)IOA), ioe = (unsigned)dpp_rol1((int)IOE), ior = (unsigned)dpp_rol1((int)IOR);
         const u16x2 aL0 = as16((unsigned)dpp_shr1((int)IOA, (int)as32(aPrev[W - 1])));
         const u16x2 ehL0 = as16((unsigned)dpp_shr1((int)IOE, (int)as32(eh[W - 1])));
-        const unsigned rL0 = (unsigned)dpp_shr1((int)IOR, (int)r[W - 1]);
+        constexpr int s0 = (W - S % W) % W;     // slot of position 0 (= last step's position W-1)
+        r[s0] = (unsigned)dpp_shr1((int)IOR, (int)r[s0]);
         const u16x2 hgL0 = vsubs2(aL0, gom2);   // H - G_INIT of the left neighbour, from its A
         u16x2 tOdd = splat2(0);                 // M3: t of position p+1, folded with p's into M
 #pragma unroll
@@ -735,7 +741,7 @@ struct StripDuo {
             const int q = p > 0 ? p - 1 : 0;
             const u16x2 hgL = p > 0 ? hg[q] : hgL0;
             const u16x2 ehL = p > 0 ? eh[q] : ehL0;
-            const unsigned rL = p > 0 ? r[q] : rL0;
+            const unsigned rL = r[(p + W - S % W) % W];
             const u16x2 aD = p > 0 ? aCur[q] : L0;
             const u16x2 pen = as16(__builtin_amdgcn_perm(pB[p], pA[p], rL));
             const u16x2 t = vsubs2(aD, pen);                 // max(H_diag + s, 0)
@@ -755,22 +761,31 @@ struct StripDuo {
             hg[p] = vsubs2(H, go2);
             eh[p] = vsubs2(E, ge2);
             fh[p] = vsubs2(F, ge2);
-            r[p] = rL;
         }
         L0 = aL0;
-        IOA = l63 ? as32(aCur[W - 1]) : ioa;
-        IOE = l63 ? as32(eh[W - 1]) : ioe;
-        IOR = ior;
+        // the I/O registers move down one lane (wave_shl:1); lane 63, which has no
+        // source, keeps the 'old' operand: this step's right-edge outflow (no select)
+        IOA = (unsigned)__builtin_amdgcn_update_dpp((int)as32(aCur[W - 1]), (int)IOA, DPP_WAVE_SHL1, 0xF, 0xF, false);
+        IOE = (unsigned)__builtin_amdgcn_update_dpp((int)as32(eh[W - 1]), (int)IOE, DPP_WAVE_SHL1, 0xF, 0xF, false);
+        IOR = (unsigned)__builtin_amdgcn_mov_dpp((int)IOR, DPP_WAVE_SHL1, 0xF, 0xF, true);
+    }
+
+    // steps K, K+1, ... of an unrolled group of U = max(W, 2): slot rotation by S = K mod W,
+    // A ping-pong by K mod 2
+    template <int K, int U>
+    __device__ __forceinline__ void steps(const u16x2 go2, const u16x2 ge2, const u16x2 ma2, const u16x2 gom2) {
+        if constexpr (K < U) {
+            if constexpr (K % 2 == 0) step<K % W>(aA, aB, go2, ge2, ma2, gom2);
+            else step<K % W>(aB, aA, go2, ge2, ma2, gom2);
+            steps<K + 1, U>(go2, ge2, ma2, gom2);
+        }
     }
 
     template <int C>
-    __device__ __forceinline__ void run(const bool l63, const u16x2 go2, const u16x2 ge2, const u16x2 ma2,
-                                        const u16x2 gom2) {
-#pragma unroll 2
-        for (int s = 0; s < C; s += 2) {
-            step(aA, aB, l63, go2, ge2, ma2, gom2);
-            step(aB, aA, l63, go2, ge2, ma2, gom2);
-        }
+    __device__ __forceinline__ void run(const u16x2 go2, const u16x2 ge2, const u16x2 ma2, const u16x2 gom2) {
+        constexpr int U = W < 2 ? 2 : W;
+        static_assert(C % U == 0, "a chunk is a whole number of slot rotations");
+        for (int s = 0; s < C; s += U) steps<0, U>(go2, ge2, ma2, gom2);
     }
 
     __device__ __forceinline__ void commit_max(const KParams& kp, const DuoDesc& d, int lane) {
@@ -800,7 +815,6 @@ template <int W, int C, bool M3>
 __device__ void strip_pass_duo(const KParams& kp, const DuoDesc& d, const int strip, const int lane) {
     constexpr int SW = 64 * W;
     const int m = d.m_pad;
-    const bool l63 = lane == 63;
     const u16x2 go2 = splat2(kp.gap_init), ge2 = splat2(kp.gap_ext), ma2 = splat2(kp.match),
                 gom2 = splat2(kp.gap_init + kp.match);
     StripDuo<W, M3> S;
@@ -834,7 +848,7 @@ __device__ void strip_pass_duo(const KParams& kp, const DuoDesc& d, const int st
             S.IOE = real ? g.z : 0u;
             S.IOR = code;
         }
-        S.template run<C>(l63, go2, ge2, ma2, gom2);
+        S.template run<C>(go2, ge2, ma2, gom2);
         if (has_out) publish_granules<W, C>(kp.epoch, out_rsrc, k0, lane, m, (int)S.IOA, (int)S.IOE);
     }
     S.commit_max(kp, d, lane);
