@@ -511,7 +511,8 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
     const int items = job.item_base[np];
     long long blocks = g_opt_blocks.load();
     if (blocks <= 0) {
-        const long long cap = (long long)c->cus * std::max(1, wpc / 4);
+        const int wpb = job.mode == MODE_DUO ? DUO_WAVES : 4;   // waves per workgroup
+        const long long cap = (long long)c->cus * std::max(1, wpc / wpb);
         // strip mode: 4 independent waves per block; chain: one block per group;
         // pair-per-workgroup: one block per pair (grid-stride over pairs)
         const long long want = job.mode == MODE_STRIP ? (items + 3) / 4 : grouped_mode(job.mode) ? items : (long long)np;   // pairwg/duo: np workgroups

@@ -855,24 +855,26 @@ __device__ void strip_pass_duo(const KParams& kp, const DuoDesc& d, const int st
 }
 
 // Kernel 4 (DNA batches, 16-bit scores): workgroup b scores duos b, b+gridDim,
-// ...; wave w runs strips w, w+4, ... of each duo (as sw_pairwg_kernel).
+// ...; its DUO_WAVES waves run strips w, w+DUO_WAVES, ... of each duo (as
+// sw_pairwg_kernel).  Four waves: eight (four per SIMD at C3) measured 3% slower
+// (12.43 vs 12.06 ms), so the step is issue-bound, not latency-bound.
 // M3: H = max3 and the running max fold two positions per v_pk_maximum3_f16
 // (scores below 0x7C00 only, LaunchCfg::duo_f16).
 template <int W, int C, bool M3>
-__global__ void __launch_bounds__(256) sw_duo_kernel(KParams kp) {
+__global__ void __launch_bounds__(64 * DUO_WAVES) sw_duo_kernel(KParams kp) {
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     for (int di = blockIdx.x; di < kp.npairs; di += gridDim.x) {
         const DuoDesc d = load_duo(kp, di);
-        for (int strip = wave; strip < d.strips; strip += 4) strip_pass_duo<W, C, M3>(kp, d, strip, lane);
+        for (int strip = wave; strip < d.strips; strip += DUO_WAVES) strip_pass_duo<W, C, M3>(kp, d, strip, lane);
     }
 }
 
 template <class K>
-int occupancy_waves(K kernel) {
+int occupancy_waves(K kernel, int threads = 256) {
     int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)kernel, 256, 0) != hipSuccess) return 4;
-    return nb * 4;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)kernel, threads, 0) != hipSuccess) return 4;
+    return nb * threads / 64;
 }
 
 template <int W, int C, bool DNA>
@@ -898,8 +900,8 @@ hipError_t launch_t(const LaunchCfg& cfg, const KParams& kp, hipStream_t s) {
             return hipErrorInvalidValue;
         case MODE_DUO:
             if constexpr (DNA) {
-                if (cfg.duo_f16) hipLaunchKernelGGL((sw_duo_kernel<W, C, true>), dim3(cfg.blocks), dim3(256), 0, s, kp);
-                else hipLaunchKernelGGL((sw_duo_kernel<W, C, false>), dim3(cfg.blocks), dim3(256), 0, s, kp);
+                if (cfg.duo_f16) hipLaunchKernelGGL((sw_duo_kernel<W, C, true>), dim3(cfg.blocks), dim3(64 * DUO_WAVES), 0, s, kp);
+                else hipLaunchKernelGGL((sw_duo_kernel<W, C, false>), dim3(cfg.blocks), dim3(64 * DUO_WAVES), 0, s, kp);
                 break;
             }
             return hipErrorInvalidValue;
@@ -918,7 +920,7 @@ int waves_t(int mode) {
             if constexpr (DNA) return occupancy_waves(sw_flow_kernel<W, C>);
             return 0;
         case MODE_DUO:
-            if constexpr (DNA) return occupancy_waves(sw_duo_kernel<W, C, true>);
+            if constexpr (DNA) return occupancy_waves(sw_duo_kernel<W, C, true>, 64 * DUO_WAVES);
             return 4;
         default: return 4;
     }
