@@ -23,7 +23,7 @@ __all__ = [
     "SmithWatermanScoreCUDA", "SmithDiagonalGPU", "score", "score_batch", "score_batch_device",
     "set_params", "get_params", "set_option", "get_option", "last_stats", "gen_pair", "gen_batch",
     "SwError", "LIB_PATH", "SW_FLAG_DNA", "SW_FLAG_BYTES", "slab_bounds", "SlabBuffer", "slab_alloc",
-    "ipc_open", "ipc_close", "score_slab_device",
+    "ipc_open", "ipc_close", "score_slab_device", "Database",
 ]
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -118,6 +118,25 @@ def lib() -> ctypes.CDLL:
     L.sw_ipc_open.restype = i
     L.sw_ipc_close.argtypes = [vp]
     L.sw_ipc_close.restype = i
+    # FASTA databases (include/algoGPU.h)
+    L.sw_db_open.argtypes = [ctypes.c_char_p]
+    L.sw_db_open.restype = vp
+    L.sw_db_from_fasta.argtypes = [ctypes.c_char_p, ctypes.c_longlong]
+    L.sw_db_from_fasta.restype = vp
+    L.sw_db_save.argtypes = [vp, ctypes.c_char_p]
+    L.sw_db_save.restype = i
+    L.sw_db_count.argtypes = [vp]
+    L.sw_db_count.restype = i
+    L.sw_db_residues.argtypes = [vp]
+    L.sw_db_residues.restype = ctypes.c_longlong
+    L.sw_db_record.argtypes = [vp, i, ctypes.POINTER(u8p), ctypes.POINTER(i), ctypes.POINTER(ctypes.c_char_p)]
+    L.sw_db_record.restype = i
+    L.sw_db_search.argtypes = [vp, u8p, i, ctypes.POINTER(i)]
+    L.sw_db_search.restype = i
+    L.sw_db_search_db.argtypes = [vp, vp, ctypes.POINTER(i)]
+    L.sw_db_search_db.restype = i
+    L.sw_db_close.argtypes = [vp]
+    L.sw_db_close.restype = None
     _lib = L
     return L
 
@@ -315,3 +334,6 @@ def gen_batch(seed_base: int, npairs: int, length: int) -> np.ndarray:
     arena = np.empty(2 * length * npairs, dtype=np.uint8)
     lib().sw_gen_batch(seed_base, npairs, length, _ptr(arena))
     return arena
+
+
+from .db import Database  # noqa: E402  (FASTA databases, query x database search)

@@ -704,6 +704,10 @@ __global__ void alphabet_kernel(const unsigned char* arena, const PairDesc* pair
 }
 
 }  // namespace
+
+// the thread's sw_last_error() text, for the other host modules (sw_db.hip)
+void report_error(const char* msg) { set_err("%s", msg); }
+
 }  // namespace swmi
 
 using namespace swmi;

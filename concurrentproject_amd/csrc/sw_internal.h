@@ -136,6 +136,9 @@ __host__ __device__ constexpr int flow2_stage_bytes(int m, int C) {
 }
 __host__ __device__ constexpr int flow2_static_lds(int C) { return 4 * 256 * 8 + 4 * 64 * 8 + 4 * 64 * 4 + 64 + 0 * C; }
 __host__ __device__ constexpr int flow2_stage_max(int C) { return LDS_PER_CU - flow2_static_lds(C) - 256; }
+// sets the calling thread's sw_last_error() text (sw_engine.hip)
+void report_error(const char* msg);
+
 hipError_t launch_sw_flow2(const LaunchCfg& cfg, const KParams& kp, hipStream_t stream);
 int flow2_waves_per_cu(int C);
 bool flow2_variant_exists(int C);

@@ -114,6 +114,38 @@ int sw_slab_free(void* d_buf);
 int sw_ipc_open(const void* ipc_handle, void** d_ptr);
 int sw_ipc_close(void* d_ptr);
 
+/* ---- FASTA databases: query x database scoring (no reference counterpart;
+ * SURVEY.md 8(f) f-4, the makedb / align workflow of the reference's timing.sh:3-8
+ * around the external CUDASW++4 tool, Makefile_CUDASW4.mak:44-56) ------------
+ * Scores are this engine's (byte equality MATCH/MISMATCH, affine gaps,
+ * main.cpp:28-66), not CUDASW++'s BLOSUM62.  A database holds its residues
+ * host-side and, after the first search, once in device memory (one arena,
+ * per device); searches launch one batch over all of its records, longest
+ * first, and return the scores in record order.
+ *
+ * sw_db_open: a FASTA file ('>' header lines; sequence lines of any width,
+ *   whitespace and '\r' dropped, bytes otherwise kept as they are; ';' comment
+ *   lines skipped; records may be empty) or a file written by sw_db_save.
+ *   NULL on error (sw_last_error).
+ * sw_db_from_fasta: the same parse over a buffer in memory.
+ * sw_db_save: the binary database (the "makedb" step), 0 or -1.
+ * sw_db_count / sw_db_residues: records, total residues.
+ * sw_db_record: record i's residues, length and header (pointers owned by db).
+ * sw_db_search: scores_out[i] = score(query, record i) for every record; the
+ *   query is a byte string of qlen bytes.  Synchronous; 0 or -1.
+ * sw_db_search_db: scores_out[q * count(db) + i] for every record q of queries.
+ * sw_db_close: frees host and device memory. */
+typedef struct sw_db sw_db;
+sw_db* sw_db_open(const char* path);
+sw_db* sw_db_from_fasta(const char* text, long long nbytes);
+int sw_db_save(const sw_db* db, const char* path);
+int sw_db_count(const sw_db* db);
+long long sw_db_residues(const sw_db* db);
+int sw_db_record(const sw_db* db, int i, const unsigned char** seq, int* len, const char** header);
+int sw_db_search(sw_db* db, const unsigned char* query, int qlen, int* scores_out);
+int sw_db_search_db(sw_db* db, const sw_db* queries, int* scores_out);
+void sw_db_close(sw_db* db);
+
 /* Tuning knobs (process-wide).  Keys:
  *   "W"        columns per lane: 0 = auto, 1, 2, 4, 8
  *   "C"        rows per strip hand-off chunk: 0 = auto, 16, 32, 64

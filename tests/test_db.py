@@ -1,0 +1,187 @@
+"""FASTA databases and query x database search (include/algoGPU.h sw_db_*).
+
+CPU: the library's FASTA parse against a plain-Python parse written here, the
+binary database round trip and its error paths.  GPU: every search score equals
+the oracle's restatement of main.cpp (bit-exact), for DNA, protein-letter and
+mixed databases, empty records, non-default constants, many queries and the
+align / makedb command lines."""
+import os
+
+import numpy as np
+import pytest
+
+AA = np.frombuffer(b"ACDEFGHIKLMNPQRSTVWY", np.uint8)
+ACGT = np.frombuffer(b"ACGT", np.uint8)
+
+
+def py_fasta(text: bytes):
+    """The parse the library implements, restated: '>' starts a record, ';' lines
+    are comments, whitespace and CR inside sequence lines are dropped."""
+    recs = []
+    for line in text.split(b"\n"):
+        if line.startswith(b">"):
+            recs.append([line[1:].rstrip(b"\r"), bytearray()])
+        elif line.startswith(b";"):
+            continue
+        else:
+            s = bytes(c for c in line if c not in b" \t\r\v\f")
+            if s:
+                assert recs, "data before the first header"
+                recs[-1][1] += s
+    return [(h.decode("latin-1"), bytes(s)) for h, s in recs]
+
+
+def random_db(rng, nrec, alphabet, max_len, empty_every=0):
+    recs = []
+    for i in range(nrec):
+        n = 0 if empty_every and i % empty_every == 0 else int(rng.integers(1, max_len + 1))
+        recs.append(("rec%d len=%d" % (i, n), alphabet[rng.integers(0, len(alphabet), n)].tobytes()))
+    return recs
+
+
+def to_fasta(recs, width=60, crlf=False):
+    nl = b"\r\n" if crlf else b"\n"
+    out = []
+    for h, s in recs:
+        out.append(b">" + h.encode("latin-1") + nl)
+        for i in range(0, len(s), width):
+            out.append(s[i:i + width] + nl)
+    return b"".join(out)
+
+
+@pytest.fixture(scope="module")
+def sw():
+    import concurrentproject_amd as sw
+    sw.lib()
+    return sw
+
+
+# ---- CPU: parse, database file -------------------------------------------------------
+
+@pytest.mark.parametrize("text", [
+    b">a\nACGT\n>b\n\n>c\nAC\nGT",                      # no trailing newline, empty record
+    b";comment\n>x y z\r\nAC GT\r\n\tTT\r\n>y\r\n",       # CRLF, whitespace, comment, empty last
+    b"\n\n>only\nMKVLAAGIVG\nXBZ*-\n",                   # blank lines first; any bytes kept
+    b">lower\nacgtNNN\n>\nA\n",                          # lower case kept; empty header
+    b"",                                                 # empty database
+])
+def test_parse_matches_python(sw, text):
+    db = sw.Database.from_fasta(text)
+    ref = py_fasta(text)
+    assert len(db) == len(ref)
+    assert [db.record(i) for i in range(len(db))] == ref
+    assert db.residues == sum(len(s) for _, s in ref)
+
+
+def test_parse_random_widths(sw):
+    rng = np.random.default_rng(7)
+    recs = random_db(rng, 50, AA, 700, empty_every=9)
+    for width, crlf in ((60, False), (80, True), (1, False), (10000, False)):
+        db = sw.Database.from_fasta(to_fasta(recs, width, crlf))
+        assert [db.record(i) for i in range(len(db))] == recs
+
+
+def test_database_file_round_trip(sw, tmp_path):
+    rng = np.random.default_rng(8)
+    recs = random_db(rng, 40, ACGT, 500, empty_every=7)
+    fa = tmp_path / "db.fasta"
+    fa.write_bytes(to_fasta(recs))
+    db = sw.Database.open(fa)
+    out = tmp_path / "db.swdb"
+    db.save(out)
+    db2 = sw.Database.open(out)
+    assert [db2.record(i) for i in range(len(db2))] == recs
+    assert db2.residues == db.residues
+    # the makedb command line writes the same file
+    from concurrentproject_amd import makedb
+    assert makedb.main([str(fa), str(tmp_path / "cli.swdb")]) == 0
+    assert (tmp_path / "cli.swdb").read_bytes() == out.read_bytes()
+
+
+def test_database_errors(sw, tmp_path):
+    with pytest.raises(sw.SwError, match="before the first"):
+        sw.Database.from_fasta(b"ACGT\n>x\nA\n")
+    with pytest.raises(sw.SwError, match="cannot read"):
+        sw.Database.open(tmp_path / "missing.fasta")
+    db = sw.Database.from_fasta(b">a\nACGT\n>b\nGG\n")
+    db.save(tmp_path / "ok.swdb")
+    blob = (tmp_path / "ok.swdb").read_bytes()
+    (tmp_path / "cut.swdb").write_bytes(blob[:-1])
+    with pytest.raises(sw.SwError, match="truncated"):
+        sw.Database.open(tmp_path / "cut.swdb")
+    with pytest.raises(sw.SwError, match="no such record"):
+        db.record(2)
+
+
+# ---- GPU: search parity ---------------------------------------------------------------
+
+def _expect(oracle_mod, query, recs, params=None):
+    p = params or oracle_mod.Params()
+    return [oracle_mod.score_linear(query, s, p) if len(s) and len(query) else 0 for _, s in recs]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("alphabet,max_len,nrec", [("dna", 1500, 120), ("aa", 900, 150), ("mixed", 2500, 60)])
+def test_search_matches_oracle(engine, oracle_mod, alphabet, max_len, nrec):
+    rng = np.random.default_rng({"dna": 1, "aa": 2, "mixed": 3}[alphabet])
+    if alphabet == "mixed":
+        recs = random_db(rng, nrec // 2, ACGT, max_len, empty_every=5) + random_db(rng, nrec // 2, AA, max_len)
+    else:
+        recs = random_db(rng, nrec, ACGT if alphabet == "dna" else AA, max_len, empty_every=11)
+    db = engine.Database.from_records(recs)
+    for qlen in (1, 37, 640, 3000):
+        src = ACGT if alphabet != "aa" else AA
+        q = src[rng.integers(0, len(src), qlen)].tobytes()
+        got = db.search(q)
+        assert got.tolist() == _expect(oracle_mod, q, recs)
+    # a query taken from the database scores its own record at least len * MATCH
+    i = next(k for k, (_, s) in enumerate(recs) if len(s) > 100)
+    assert db.search(recs[i][1])[i] == len(recs[i][1])
+    assert db.search(b"").tolist() == [0] * len(recs)
+
+
+@pytest.mark.gpu
+def test_search_params_and_many_queries(engine, oracle_mod, tmp_path):
+    rng = np.random.default_rng(4)
+    recs = random_db(rng, 80, AA, 600, empty_every=13)
+    queries = random_db(rng, 5, AA, 400)
+    db = engine.Database.from_records(recs)
+    qs = engine.Database.from_records(queries)
+    p = engine.Params(2, -3, 5, 2)
+    engine.set_params(p)
+    try:
+        got = db.search_db(qs)
+        op = oracle_mod.Params(2, -3, 5, 2)
+        assert got.tolist() == [_expect(oracle_mod, q, recs, op) for _, q in queries]
+    finally:
+        engine.set_params(engine.Params())
+    # top-k and the align command line on the same data, default constants
+    sc = db.search(queries[0][1])
+    top = db.top(queries[0][1], k=5)
+    assert [t[0] for t in top] == sorted(sc.tolist(), reverse=True)[:5]
+    fa_db, fa_q = tmp_path / "db.fa", tmp_path / "q.fa"
+    fa_db.write_bytes(to_fasta(recs))
+    fa_q.write_bytes(to_fasta(queries))
+    from concurrentproject_amd import align
+    import contextlib
+    import io
+    buf = io.StringIO()
+    with contextlib.redirect_stdout(buf):
+        assert align.main(["--query", str(fa_q), "--db", str(fa_db), "--top", "3"]) == 0
+    lines = [ln.split("\t") for ln in buf.getvalue().splitlines()]
+    assert len(lines) == 3 * len(queries)
+    for qi, _, rank, score, idx, _hdr in lines:
+        ref = _expect(oracle_mod, queries[int(qi)][1], [recs[int(idx)]])[0]
+        assert int(score) == ref
+    first = [ln for ln in lines if ln[0] == "0"]
+    assert [int(x[3]) for x in first] == [t[0] for t in top[:3]]
+
+
+@pytest.mark.gpu
+def test_search_dna_duo_path(engine, oracle_mod):
+    """Equal-length DNA records (the packed 16-bit kernel's batch shape)."""
+    rng = np.random.default_rng(5)
+    recs = [("r%d" % i, ACGT[rng.integers(0, 4, 2048)].tobytes()) for i in range(64)]
+    db = engine.Database.from_records(recs)
+    q = ACGT[rng.integers(0, 4, 2048)].tobytes()
+    assert db.search(q).tolist() == _expect(oracle_mod, q, recs)
