@@ -1,0 +1,51 @@
+"""Database-search rate (f-4): one query against a synthetic FASTA of ragged DNA records.
+
+Times ``Database.search`` (sw_db_search, synchronous: query H2D + one batch launch over every record + score D2H),
+so the figure is host-API GCUPS, not kernel-only.  Records are uniform ACGT with lengths drawn uniformly from
+[lo, hi]; the arena is uploaded to HBM by the first (untimed) search.
+
+    python tools/bench_db.py [--records R] [--qlen Q] [--lo L] [--hi H] [--steps K]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from concurrentproject_amd.db import Database  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--records", type=int, default=65536)
+    ap.add_argument("--qlen", type=int, default=1024)
+    ap.add_argument("--lo", type=int, default=256)
+    ap.add_argument("--hi", type=int, default=4096)
+    ap.add_argument("--steps", type=int, default=10)
+    a = ap.parse_args()
+    rng = np.random.default_rng(4)
+    acgt = np.frombuffer(b"ACGT", dtype=np.uint8)
+    lens = rng.integers(a.lo, a.hi + 1, size=a.records)
+    parts = []
+    for i, n in enumerate(lens):
+        parts.append(b">r%d\n" % i + acgt[rng.integers(0, 4, size=n)].tobytes() + b"\n")
+    db = Database.from_fasta(b"".join(parts))
+    q = acgt[rng.integers(0, 4, size=a.qlen)]
+    db.search(q)  # upload + warm
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        sc = db.search(q)
+    dt = (time.perf_counter() - t0) / a.steps
+    cells = int(lens.sum()) * a.qlen
+    print(json.dumps({"metric": "db search GCUPS (host API, synchronous)", "value": round(cells / dt / 1e9, 2),
+                      "unit": "GCUPS", "ms_per_search": round(dt * 1e3, 3), "records": a.records,
+                      "residues": int(lens.sum()), "qlen": a.qlen, "len_range": [a.lo, a.hi],
+                      "max_score": int(sc.max())}))
+    db.close()
+
+
+if __name__ == "__main__":
+    main()
