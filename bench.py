@@ -1,26 +1,38 @@
 #!/usr/bin/env python3
 """Benchmark of the MI355X Smith-Waterman score path (BASELINE.json metric: GCUPS).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload auto|pair|batch]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload auto|pair|batch|slab]
 
 Workloads (BASELINE.json configs; synthetic uniform {A,C,G,T}, generator of
 cudaSmithM.cu:200-212, sequences resident in HBM before the timed region):
-  pair   C2: one pair N=65536 (seed 65536), one launch per step.  A single pair
-         does not shard; with --gpus N the global batch is N such pairs (seeds
-         65536+k), one per rank, with the per-pair scores gathered to rank 0
-         over RCCL every step.
+  pair   C2: one pair N=65536 (seed 65536), one launch per step.  With --gpus N
+         the global batch is N such pairs (seeds 65536+k), one per rank, the
+         per-pair scores gathered to rank 0 over RCCL every step.
   batch  C3/C4: 1024 pairs of N=8192 per GPU; rank r scores pairs
          [1024r, 1024r+1024) (seeds 8192+k), then the per-pair int32 scores are
          gathered to rank 0 with RCCL (torch.distributed "nccl") every step.
-  auto   pair at every --gpus (configs[1], the metric's config), so the per-N
-         values of a scaling series measure the same work per GPU; the C4
-         batch (configs[3]) is --workload batch --gpus 8.
+         --gpus 8 is config C4 (8192 pairs).
+  slab   C5: one pair N=2^20 (seed 1048576); with --gpus N its columns are cut
+         into one slab per rank (dist.ColumnSlabs).
+  auto   N=1: C2 (configs[1], the metric's single-GPU config), and the C3 batch
+         measured after it as the extra key "batch_c3".  N>1: the C4 batch
+         (configs[3]: the >= 7.5x target of north_star is stated on batched pairs).
 A step is one full pass of the hot path over the step's input; `value` is the
 whole-job GCUPS (sum of n*m over all ranks' pairs / max-over-ranks time).
+
+Roofline: the kernels keep H/E/F in registers, so the bound
+that applies is VALU issue, not HBM.  `roofline.achieved` = VALU lane-ops of one
+launch (rocprofv3 SQ_INSTS_VALU x 64, profiles/pmc_<workload>.json, valid only
+for the same libswmi355.so, checked by sha256) / the launch time measured here;
+`peak` = 256 CU x 4 SIMD x 64 lanes / 2 cycles x 2.4 GHz.  For the single pair
+`critical_path_frac` = (n+m-1) x the step time measured in this run (strip 0
+of a traced launch) / the launch time.  `traffic` = HBM bytes per launch from
+the FETCH_SIZE / WRITE_SIZE passes of the same profile.
 """
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
 import sys
@@ -33,6 +45,9 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 ALGO_BYTES_PER_CELL = 12       # int32 H, E, F produced per cell
+# VALU issue peak: 256 CUs x 4 SIMDs, one wave64 VALU instruction per SIMD every 2
+# cycles (32 lanes/clk, MI355X_MICROARCH.md "v_fma_f32 2 cyc (SIMD-32)"), 2.4 GHz
+VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12   # T lane-ops/s = 78.64
 
 
 def parse():
@@ -47,6 +62,7 @@ def parse():
     ap.add_argument("--pairs-per-gpu", type=int, default=1024)
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU baseline leg")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extra", action="store_true", help="N=1 auto: skip the extra C3 batch measurement")
     ap.add_argument("--W", type=int, default=0)
     ap.add_argument("--C", type=int, default=0)
     ap.add_argument("--mode", type=int, default=-1, help="engine option 'mode' (-1 = automatic plan)")
@@ -62,11 +78,32 @@ def load_golden():
         return {}
 
 
+def lib_sha256(path):
+    h = hashlib.sha256()
+    with open(path, "rb") as f:
+        for blk in iter(lambda: f.read(1 << 20), b""):
+            h.update(blk)
+    return h.hexdigest()
+
+
+def host_cores():
+    """(threads the CPU leg may use, what the host reports).  The GPU box gives one
+    GPU's job a share of its cores: OMP_NUM_THREADS (16 there) caps the pool."""
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count() or 1
+    cap = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return (min(avail, cap) if cap > 0 else avail), {"nproc": os.cpu_count(), "affinity": avail,
+                                                      "omp_num_threads": cap or None}
+
+
 def cpu_baseline(kind: str, n: int, budget_s: float, params):
     """The reference's sequential CPU path (main.cpp:40-90, full matrix) restated in
     oracle/sw_oracle.c, timed on a bounded sample of the same workload."""
     import oracle  # the checker / baseline leg only
     p = oracle.Params(*params)
+    threads, host = host_cores()
     if kind == "pair":
         a, b = oracle.gen_pair(65536, 65536) if n == 65536 else oracle.gen_pair(65536, n)
         rows, spent, cells, t_tot = 128, 0.0, 0, 0.0
@@ -78,9 +115,10 @@ def cpu_baseline(kind: str, n: int, budget_s: float, params):
             if spent > budget_s or rows >= len(b):
                 break
             rows = min(len(b), rows * 2)
-        return {"value": cells / t_tot / 1e9, "unit": "GCUPS", "cores": 1, "kind": "port",
+        return {"value": cells / t_tot / 1e9, "unit": "GCUPS", "cores": 1, "kind": "port", "host": host,
                 "sample": "main.cpp SmithWatermanScore restated (full (m+1)x(n+1)x3 int32 matrices), "
-                          "1 thread, on row prefixes of the C2 pair up to %d x %d; %.1f s" % (rows, len(a), t_tot)}
+                          "1 thread as in the reference, on row prefixes of the C2 pair up to %d x %d; %.1f s"
+                          % (rows, len(a), t_tot)}
     if kind == "slab":
         # C5: main.cpp's full matrices would need 13.2 TB; lazySmith.cpp's linear-space
         # restatement on row prefixes of the C5 pair
@@ -94,19 +132,136 @@ def cpu_baseline(kind: str, n: int, budget_s: float, params):
             if spent > budget_s or rows >= len(b):
                 break
             rows = min(len(b), rows * 2)
-        return {"value": cells / t_tot / 1e9, "unit": "GCUPS", "cores": 1, "kind": "port",
+        return {"value": cells / t_tot / 1e9, "unit": "GCUPS", "cores": 1, "kind": "port", "host": host,
                 "sample": "lazySmith.cpp LazySmith restated (linear space; main.cpp's matrices need 13.2 TB), "
                           "1 thread, on row prefixes of the C5 pair up to %d x %d; %.1f s" % (rows, len(a), t_tot)}
-    # batch: one pair per thread (embarrassingly parallel), a bounded subset of pairs
-    threads = max(1, min(16, os.cpu_count() or 1))
+    # batch: one pair per thread (embarrassingly parallel) on every core the job has
     npairs = threads
     pairs = [oracle.gen_pair(8192 + k, n) for k in range(npairs)]
     t0 = time.perf_counter()
     oracle.score_batch(pairs, p, threads=threads, full=True)
     dt = time.perf_counter() - t0
-    return {"value": npairs * n * n / dt / 1e9, "unit": "GCUPS", "cores": threads, "kind": "port",
-            "sample": "main.cpp SmithWatermanScore restated (full matrices), one pair per thread, "
-                      "%d pairs of %d x %d (seeds 8192+k); %.1f s" % (npairs, n, n, dt)}
+    return {"value": npairs * n * n / dt / 1e9, "unit": "GCUPS", "cores": threads, "kind": "port", "host": host,
+            "sample": "main.cpp SmithWatermanScore restated (full matrices), one pair per thread on all %d cores "
+                      "of this job, %d pairs of %d x %d (seeds 8192+k); %.1f s" % (threads, npairs, n, n, dt)}
+
+
+def profile_for(workload):
+    """profiles/pmc_<workload>.json when it was taken with THIS library build."""
+    import concurrentproject_amd as sw
+    path = os.path.join(ROOT, "profiles", "pmc_%s.json" % workload)
+    if not os.path.exists(path):
+        return None, "no profile"
+    try:
+        prof = json.load(open(path))
+    except Exception as e:
+        return None, repr(e)
+    if prof.get("lib_sha256") != lib_sha256(sw.LIB_PATH):
+        return None, "stale: profile taken with another libswmi355.so build"
+    return prof, os.path.relpath(path, ROOT)
+
+
+def roofline(workload, per_launch_cells, avg_kern_ms, step_ns=None, n=0, m=0):
+    prof, src = profile_for(workload)
+    t = avg_kern_ms * 1e-3
+    out = {"bound": "valu", "unit": "Tlane-ops/s", "peak": round(VALU_PEAK_TOPS, 2), "achieved": None, "frac": None,
+           "traffic": None, "source": src}
+    if prof is not None and prof.get("valu_insts_per_launch"):
+        ops = prof["valu_insts_per_launch"] * 64
+        out["achieved"] = round(ops / t / 1e12, 3)
+        out["frac"] = round(ops / t / 1e12 / VALU_PEAK_TOPS, 4)
+        out["valu_lane_ops_per_launch"] = ops
+        out["valu_insts_per_cell"] = round(prof["valu_insts_per_launch"] * 64 / per_launch_cells, 3)
+    if prof is not None:
+        out["traffic"] = prof.get("hbm_bytes_per_launch")
+        if prof.get("clock_ghz"):
+            out["profiled_clock_ghz"] = prof["clock_ghz"]
+    algo = per_launch_cells * ALGO_BYTES_PER_CELL
+    out["hbm"] = {"algorithmic_bytes_per_launch": algo,
+                  "algorithmic_frac": round(algo / t / 1e9 / HBM_PEAK_GBS, 4),
+                  "traffic_frac": (round(out["traffic"] / t / 1e9 / HBM_PEAK_GBS, 4) if out["traffic"] else None),
+                  "note": "12 B/cell (int32 H, E, F, SURVEY 8d) is notional: the kernel keeps them on chip, so "
+                          "algorithmic_frac can exceed 1; traffic_frac is the counted HBM bytes"}
+    if step_ns:
+        out["step_ns"] = round(step_ns, 3)
+        out["critical_path_frac"] = round((n + m - 1) * step_ns / (avg_kern_ms * 1e6), 4)
+    return out
+
+
+def measure_step_ns(sw, torch, arena, offs_a, lens, offs_b, scores, sptr, N):
+    """Step time of the single-pair kernel's first strip (no inflow: its own pace)
+    from one traced launch: (end - start) / (m + 63) steps, s_memrealtime 100 MHz."""
+    st = sw.last_stats()
+    if st["mode"] != 5:
+        return None
+    strips = max(1, (N - 1 + 62) // 63)
+    trace = torch.zeros(16 * strips, dtype=torch.int64, device="cuda")
+    sw.set_option("trace", trace.data_ptr())
+    try:
+        sw.score_batch_device(arena.data_ptr(), offs_a, lens, offs_b, lens, scores.data_ptr(), flags=1, stream=sptr)
+        torch.cuda.synchronize()
+    finally:
+        sw.set_option("trace", 0)
+    sw.stream_status(sptr)
+    t = trace.cpu().numpy().reshape(strips, 16)
+    return float(t[0, 2] - t[0, 0]) * 10.0 / (N + 63)
+
+
+def time_launches(torch, launch, collective, steps, warmup, stream, dist):
+    for _ in range(warmup):
+        launch()
+        collective()
+    torch.cuda.synchronize()
+    starts = [torch.cuda.Event(enable_timing=True) for _ in range(steps)]
+    ends = [torch.cuda.Event(enable_timing=True) for _ in range(steps)]
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        starts[i].record(stream)
+        launch()
+        ends[i].record(stream)
+        collective()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    t_local = time.perf_counter() - t0
+    kern_ms = float(np.mean([s.elapsed_time(e) for s, e in zip(starts, ends)]))
+    t_max = t_local
+    if dist is not None:
+        tt = torch.tensor([t_local], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        t_max = float(tt.item())
+    return t_max, kern_ms
+
+
+def run_batch(sw, torch, dist, world, rank, N, P, steps, warmup):
+    """C3 (one GPU) / C4 (sharded): rank r scores its contiguous block of the global
+    batch, then the per-pair scores are gathered to rank 0 (RCCL) every step."""
+    from concurrentproject_amd.dist import gather_scores, shard_bounds
+    lo, hi = shard_bounds(P * world, world, rank)
+    host = sw.gen_batch(8192 + lo, hi - lo, N)
+    npairs = hi - lo
+    arena = torch.from_numpy(host).cuda()
+    scores = torch.zeros(npairs, dtype=torch.int32, device="cuda")
+    stream = torch.cuda.current_stream()
+    offs_a = [2 * N * k for k in range(npairs)]
+    offs_b = [2 * N * k + N for k in range(npairs)]
+    gathered = [None]
+
+    def launch():
+        sw.score_batch_device(arena.data_ptr(), offs_a, [N] * npairs, offs_b, [N] * npairs, scores.data_ptr(),
+                              flags=1, stream=stream.cuda_stream)
+
+    def collective():
+        if dist is not None:
+            gathered[0] = gather_scores(scores, P * world)
+
+    t_max, kern_ms = time_launches(torch, launch, collective, steps, warmup, stream, dist)
+    sw.stream_status(stream.cuda_stream)
+    allsc = gathered[0].cpu().tolist() if gathered[0] is not None else scores.cpu().tolist()
+    return t_max, kern_ms, allsc, npairs * N * N, sw.last_stats()
 
 
 def main():
@@ -129,186 +284,137 @@ def main():
         sw.set_option("C", args.C)
     if args.mode >= 0:
         sw.set_option("mode", args.mode)
+    gold = load_golden()
+    defaults = params == (1, -1, 1, 1)
 
     workload = args.workload
     if workload == "auto":
-        workload = "pair"   # the metric's config at every N, so the driver's per-N values compare
+        workload = "pair" if world == 1 else "batch"
 
-    if workload == "pair":
-        # C2 at N=1; at N GPUs a global batch of N such pairs (pair k seeded 65536+k),
-        # one per rank, scores gathered to rank 0 over RCCL every step (weak scaling)
-        N = args.n or 65536
-        seed = 65536 + rank
-        a, b = sw.gen_pair(seed, N)
-        host = np.concatenate([a, b])
-        offs_a, offs_b, lens = [0], [N], [N]
-        npairs_rank = 1
-        cfg = {"workload": "C2 single pair N=%d (seed 65536)" % N if world == 1 else
-                           "C2-size pairs N=%d, one per GPU (seeds 65536+rank)" % N,
-               "N": N, "pairs_per_gpu": 1, "global_pairs": world,
-               "parallelism": "pair-sharded x%d + RCCL gather of scores" % world if world > 1 else "single GPU"}
-    elif workload == "slab":
-        # C5: ONE pair N = 2^20 (seed 1048576); with --gpus N its columns are cut into
-        # one slab per rank (dist.ColumnSlabs: slab edges stored GPU to GPU through
-        # IPC-mapped buffers, all-reduce(MAX) of the score).  Every rank holds the
-        # whole pair (2 MB).  One GPU: the plain single-pair path, or with --slab-of K
-        # slab 0 of a K-way split alone (edge into a local buffer): the per-rank cost.
-        N = args.n or (1 << 20)
-        a, b = sw.gen_pair(1048576 if N == 1 << 20 else N, N)
-        host = np.concatenate([a, b])
-        offs_a, offs_b, lens = [0], [N], [N]
-        npairs_rank = 1
-        cfg = {"workload": "C5 single pair N=%d (seed 1048576)" % N, "N": N, "pairs_per_gpu": 1.0 / world,
-               "global_pairs": 1,
-               "parallelism": ("column slabs x%d, GPU-to-GPU edge stores + RCCL all-reduce(MAX)" % world
-                               if world > 1 else "single GPU")}
-    else:
-        from concurrentproject_amd.dist import shard_bounds
+    extra = None
+    step_ns = None
+    host_api = None
+    parity = "unchecked"
+    if workload == "batch":
         N = args.n or 8192
         P = args.pairs_per_gpu
-        lo, hi = shard_bounds(P * world, world, rank)   # contiguous block of the global batch
-        base = 8192 + lo
-        host = sw.gen_batch(base, hi - lo, N)
-        P = hi - lo
-        offs_a = [2 * N * k for k in range(P)]
-        offs_b = [2 * N * k + N for k in range(P)]
-        lens = [N] * P
-        npairs_rank = P
-        cfg = {"workload": ("C4 batch, %d pairs/GPU" % P) if world > 1 else "C3 batch of %d pairs" % P,
-               "N": N, "pairs_per_gpu": P, "global_pairs": P * world,
+        t_max, avg_kern_ms, allsc, cells_rank, st = run_batch(sw, torch, dist, world, rank, N, P, args.steps,
+                                                              args.warmup)
+        cells_job = cells_rank * world
+        per_launch_cells = cells_rank
+        cfg = {"workload": ("C4 batch, %d pairs/GPU (%d pairs)" % (P, P * world)) if world > 1
+               else "C3 batch of %d pairs" % P, "N": N, "pairs_per_gpu": P, "global_pairs": P * world,
                "parallelism": "pair-sharded x%d + RCCL gather of scores" % world if world > 1 else "single GPU"}
-
-    arena = torch.from_numpy(host).cuda()
-    scores = torch.zeros(npairs_rank, dtype=torch.int32, device="cuda")
-    stream = torch.cuda.current_stream()
-    sptr = stream.cuda_stream
-    gathered = None
-    total_pairs = npairs_rank * world
-
-    def gather():
-        from concurrentproject_amd.dist import gather_scores
-        return gather_scores(scores, total_pairs)     # RCCL gather of the per-pair int32 scores
-
-    # the launch of one step (the timed kernel), then the step's collective
-    slabs, slab_buf, slab_cols = None, None, None
-    cells_rank = sum(int(x) * int(y) for x, y in zip(lens, lens))
-    cells_job = cells_rank * world
-    if workload == "slab" and dist is not None:
-        from concurrentproject_amd.dist import ColumnSlabs
-        slabs = ColumnSlabs(N, N, sw.SW_FLAG_DNA)
-        lo, hi = slabs.columns
-        cells_rank, cells_job = (hi - lo) * N, N * N
-        cfg["slab_columns"] = [lo, hi]
-    elif workload == "slab" and args.slab_of > 1:
-        bounds = sw.slab_bounds(N, N, args.slab_of, sw.SW_FLAG_DNA)
-        slab_cols, slab_buf = bounds[1], sw.slab_alloc(N)
-        cells_rank = cells_job = slab_cols * N
-        cfg.update(workload="C5 slab 0 of a %d-way column split, alone (per-rank cost)" % args.slab_of,
-                   slab_columns=[0, slab_cols])
-    epoch = [0]
-
-    def launch():
-        if slabs is not None:
-            epoch[0] += 1
-            lo, hi = slabs.columns
-            sw.score_slab_device(arena.data_ptr(), lo, hi - lo, N, N, slabs.inflow.ptr if slabs.inflow else 0,
-                                 slabs.outflow, slabs.epoch + epoch[0], scores.data_ptr(), sw.SW_FLAG_DNA, sptr)
-        elif slab_buf is not None:
-            epoch[0] += 1
-            sw.score_slab_device(arena.data_ptr(), 0, slab_cols, N, N, 0, slab_buf.ptr, epoch[0],
-                                 scores.data_ptr(), sw.SW_FLAG_DNA, sptr)
-        else:
-            sw.score_batch_device(arena.data_ptr(), offs_a, lens, offs_b, lens, scores.data_ptr(),
-                                  flags=1, stream=sptr)
-
-    def collective():
-        nonlocal gathered
-        if dist is None:
-            return
-        if slabs is not None:
-            from concurrentproject_amd.dist import slab_max
-            slab_max(scores)                           # RCCL all-reduce(MAX) of one int
-        else:
-            gathered = gather()
-
-    for _ in range(args.warmup):
-        launch()
-        collective()
-    sw.stream_status(sptr)
-    torch.cuda.synchronize()
-
-    starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
-    ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        starts[i].record(stream)
-        launch()
-        ends[i].record(stream)
-        collective()
-    torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
-    t_local = time.perf_counter() - t0
-    sw.stream_status(sptr)
-    st = sw.last_stats()
-    kern_ms = [s.elapsed_time(e) for s, e in zip(starts, ends)]
-    avg_kern_ms = float(np.mean(kern_ms))
-
-    t_max = t_local
-    if dist is not None:
-        tt = torch.tensor([t_local], dtype=torch.float64, device="cuda")
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        t_max = float(tt.item())
-
-    total_cells = cells_job * args.steps
-    value = total_cells / t_max / 1e9
-    if slabs is not None:
-        slabs.close()
-    if slab_buf is not None:
-        slab_buf.free()
-
-    # PCIe-inclusive rate of the synchronous host entry point (H2D of the two
-    # sequences + launch + score D2H): reported beside `value`, never as it
-    host_api = None
-    if rank == 0 and workload == "pair":
-        a_h, b_h = host[:N], host[N:]
-        sw.SmithWatermanScoreCUDA(a_h, b_h)
-        t1 = time.perf_counter()
-        hs = sw.SmithWatermanScoreCUDA(a_h, b_h)
-        host_api = {"gcups": round(N * N / (time.perf_counter() - t1) / 1e9, 3), "score": hs,
-                    "entry": "SmithWatermanScoreCUDA (algoGPU.h:9), host buffers"}
-
-    # parity of what was just computed (scores vs the committed golden fixtures)
-    parity = "unchecked"
-    gold = load_golden()
-    if rank == 0 and params == (1, -1, 1, 1):
-        if workload == "pair" and N == 65536 and "C2" in gold:   # rank 0's pair is the C2 pair
-            first = gathered[0].item() if gathered is not None else scores[0].item()
-            parity = "ok" if first == gold["C2"]["score"] else "MISMATCH"
-        elif workload == "batch" and N == 8192:
-            allsc = gathered.cpu().tolist() if gathered is not None else scores.cpu().tolist()
+        if rank == 0 and defaults and N == 8192:
             ref = gold.get("C4", gold.get("C3", {})).get("scores", [])
             if len(ref) >= len(allsc):
                 parity = "ok" if allsc == ref[:len(allsc)] else "MISMATCH"
-        elif workload == "slab" and N == 1 << 20 and slab_buf is None:
-            # C5 has no CPU golden (~2 h single-core): the property-checked score
-            # (default plan == transposed == W=4 plan, tools/c5_check.py)
-            parity = ("ok (vs property-checked 119470, CPU-unpinned)" if scores[0].item() == 119470
-                      else "MISMATCH")
-
-    if rank == 0:
+    else:
+        slabs, slab_buf, slab_cols = None, None, None
+        if workload == "pair":
+            # C2 at N=1; at N GPUs a global batch of N such pairs (pair k seeded 65536+k)
+            N = args.n or 65536
+            a, b = sw.gen_pair(65536 + rank, N)
+            cfg = {"workload": "C2 single pair N=%d (seed 65536)" % N if world == 1 else
+                               "C2-size pairs N=%d, one per GPU (seeds 65536+rank)" % N,
+                   "N": N, "pairs_per_gpu": 1, "global_pairs": world,
+                   "parallelism": "pair-sharded x%d + RCCL gather of scores" % world if world > 1 else "single GPU"}
+        else:
+            # C5: ONE pair N = 2^20 (seed 1048576); every rank holds the whole pair (2 MB)
+            N = args.n or (1 << 20)
+            a, b = sw.gen_pair(1048576 if N == 1 << 20 else N, N)
+            cfg = {"workload": "C5 single pair N=%d (seed 1048576)" % N, "N": N, "pairs_per_gpu": 1.0 / world,
+                   "global_pairs": 1,
+                   "parallelism": ("column slabs x%d, GPU-to-GPU edge stores + RCCL all-reduce(MAX)" % world
+                                   if world > 1 else "single GPU")}
+        host = np.concatenate([a, b])
+        arena = torch.from_numpy(host).cuda()
+        scores = torch.zeros(1, dtype=torch.int32, device="cuda")
+        stream = torch.cuda.current_stream()
+        sptr = stream.cuda_stream
+        offs_a, offs_b, lens = [0], [N], [N]
+        cells_rank = cells_job = N * N
+        if workload == "slab" and dist is not None:
+            from concurrentproject_amd.dist import ColumnSlabs
+            slabs = ColumnSlabs(N, N, sw.SW_FLAG_DNA)
+            lo, hi = slabs.columns
+            cells_rank, cells_job = (hi - lo) * N, N * N
+            cfg["slab_columns"] = [lo, hi]
+        elif workload == "slab" and args.slab_of > 1:
+            bounds = sw.slab_bounds(N, N, args.slab_of, sw.SW_FLAG_DNA)
+            slab_cols, slab_buf = bounds[1], sw.slab_alloc(N)
+            cells_rank = cells_job = slab_cols * N
+            cfg.update(workload="C5 slab 0 of a %d-way column split, alone (per-rank cost)" % args.slab_of,
+                       slab_columns=[0, slab_cols])
+        elif workload == "pair":
+            cells_job = N * N * world
         per_launch_cells = cells_rank
-        achieved = per_launch_cells * ALGO_BYTES_PER_CELL / (avg_kern_ms * 1e-3) / 1e9
-        traffic = None
-        pmc_path = os.path.join(ROOT, "profiles", "pmc_%s.json" % workload)
-        if os.path.exists(pmc_path):
-            try:
-                traffic = json.load(open(pmc_path)).get("hbm_bytes_per_launch")
-            except Exception:
-                traffic = None
+        epoch = [0]
+        gathered = [None]
+
+        def launch():
+            if slabs is not None:
+                epoch[0] += 1
+                lo, hi = slabs.columns
+                sw.score_slab_device(arena.data_ptr(), lo, hi - lo, N, N, slabs.inflow.ptr if slabs.inflow else 0,
+                                     slabs.outflow, slabs.epoch + epoch[0], scores.data_ptr(), sw.SW_FLAG_DNA, sptr)
+            elif slab_buf is not None:
+                epoch[0] += 1
+                sw.score_slab_device(arena.data_ptr(), 0, slab_cols, N, N, 0, slab_buf.ptr, epoch[0],
+                                     scores.data_ptr(), sw.SW_FLAG_DNA, sptr)
+            else:
+                sw.score_batch_device(arena.data_ptr(), offs_a, lens, offs_b, lens, scores.data_ptr(),
+                                      flags=1, stream=sptr)
+
+        def collective():
+            if dist is None:
+                return
+            if slabs is not None:
+                from concurrentproject_amd.dist import slab_max
+                slab_max(scores)                           # RCCL all-reduce(MAX) of one int
+            else:
+                from concurrentproject_amd.dist import gather_scores
+                gathered[0] = gather_scores(scores, world)  # RCCL gather of the per-pair int32 scores
+
+        t_max, avg_kern_ms = time_launches(torch, launch, collective, args.steps, args.warmup, stream, dist)
+        sw.stream_status(sptr)
+        st = sw.last_stats()
+        first = gathered[0][0].item() if gathered[0] is not None else scores[0].item()
+        if slabs is not None:
+            slabs.close()
+        if slab_buf is not None:
+            slab_buf.free()
+        if rank == 0 and world == 1 and slab_buf is None:
+            step_ns = measure_step_ns(sw, torch, arena, offs_a, lens, offs_b, scores, sptr, N)
+        # PCIe-inclusive rate of the synchronous host entry point (H2D of the two
+        # sequences + launch + score D2H): reported beside `value`, never as it
+        if rank == 0 and workload == "pair":
+            a_h, b_h = host[:N], host[N:]
+            sw.SmithWatermanScoreCUDA(a_h, b_h)
+            t1 = time.perf_counter()
+            hs = sw.SmithWatermanScoreCUDA(a_h, b_h)
+            host_api = {"gcups": round(N * N / (time.perf_counter() - t1) / 1e9, 3), "score": hs,
+                        "entry": "SmithWatermanScoreCUDA (algoGPU.h:9), host buffers"}
+        if rank == 0 and defaults:
+            if workload == "pair" and N == 65536 and "C2" in gold:   # rank 0's pair is the C2 pair
+                parity = "ok" if first == gold["C2"]["score"] else "MISMATCH"
+            elif workload == "slab" and N == 1 << 20 and slab_buf is None and "C5" in gold:
+                parity = "ok" if first == gold["C5"]["score"] else "MISMATCH"
+        # N=1: the batched config (C3) measured right after, as an extra key
+        if workload == "pair" and world == 1 and args.workload == "auto" and not args.no_extra:
+            bt, bk, bsc, bcells, bst = run_batch(sw, torch, None, 1, 0, 8192, 1024, max(3, args.steps // 2), 1)
+            ref = gold.get("C4", gold.get("C3", {})).get("scores", [])
+            extra = {"workload": "C3 batch of 1024 pairs N=8192 (seeds 8192+k)", "value": round(bcells * max(3, args.steps // 2) / bt / 1e9, 3),
+                     "unit": "GCUPS", "kernel_ms_per_launch": round(bk, 4),
+                     "kernel_gcups": round(bcells / (bk * 1e-3) / 1e9, 3),
+                     "parity": ("ok" if bsc == ref[:len(bsc)] else "MISMATCH") if defaults and len(ref) >= 1024
+                     else "unchecked",
+                     "kernel": {3: "duo", 1: "pairwg"}.get(bst["mode"], bst["mode"]),
+                     "dtype": "u16x2 (packed, exact: scores < 2^16)" if bst["mode"] == 3 else "int32",
+                     "roofline": roofline("batch", bcells, bk)}
+
+    value = cells_job * args.steps / t_max / 1e9
+    if rank == 0:
         out = {
             "metric": "GCUPS (cell updates/s) for NxN affine-gap SW; bit-exact score vs CPU",
             "value": round(value, 3),
@@ -323,20 +429,21 @@ def main():
             "dtype": "u16x2 (packed, exact: scores < 2^16)" if st["mode"] == 3 else "int32",
             "data": "synthetic (uniform ACGT, mt19937_64 seeds as cudaSmithM.cu:200-212), resident in HBM",
             "config": dict(cfg, params=list(params), W=st["W"], C=st["C"], kernel_items=st["items"],
-                           blocks=st["blocks"], kernel={0: "strip", 1: "pairwg", 2: "chain", 3: "duo",
-                                                        4: "flow", 5: "flow2"}.get(st["mode"], st["mode"])),
+                           blocks=st["blocks"], boundary_bytes=st["boundary_bytes"],
+                           kernel={0: "strip", 1: "pairwg", 2: "chain", 3: "duo", 4: "flow",
+                                   5: "flow2"}.get(st["mode"], st["mode"])),
             "kernel_ms_per_launch": round(avg_kern_ms, 4),
             "kernel_gcups": round(per_launch_cells / (avg_kern_ms * 1e-3) / 1e9, 3),
             "parity": parity,
             "host_api": host_api,
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "note": "achieved = n*m*12 B (int32 H,E,F per cell, SURVEY 8d) / avg kernel time; "
-                                 "the kernel keeps H/E/F on chip, so it is VALU-bound, not HBM-bound (DESIGN.md)"},
+            "roofline": roofline(workload if args.slab_of <= 1 else "slab_part", per_launch_cells, avg_kern_ms,
+                                 step_ns, cfg["N"], cfg["N"]),
         }
+        if extra is not None:
+            out["batch_c3"] = extra
         if world == 1 and not args.no_cpu_baseline:
             try:
-                out["cpu_baseline"] = cpu_baseline(workload, N, args.cpu_seconds, params)
+                out["cpu_baseline"] = cpu_baseline(workload, cfg["N"], args.cpu_seconds, params)
             except Exception as e:   # the baseline leg must not kill the GPU number
                 out["cpu_baseline"] = {"error": repr(e)}
         print(json.dumps(out), flush=True)

@@ -58,7 +58,7 @@ _lib = None
 def build(verbose: bool = False) -> str:
     """Compile libswmi355.so in-tree for gfx950 (hipcc; no GPU needed)."""
     import subprocess
-    cmd = ["make", "-C", os.path.join(HERE, "csrc")]
+    cmd = ["make", "-j4", "-C", os.path.join(HERE, "csrc")]
     if not verbose:
         cmd.insert(1, "-s")
     subprocess.run(cmd, check=True)

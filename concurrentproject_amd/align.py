@@ -29,14 +29,14 @@ def main(argv=None) -> int:
         t0 = time.perf_counter()
         scores = db.search_db(qs)
         dt = time.perf_counter() - t0
-        cells = int(sum(len(qs.record(q)[1]) for q in range(len(qs)))) * int(lens.sum())
+        cells = int(qs.lengths().sum()) * int(lens.sum())
         out = sys.stdout
         for q in range(len(qs)):
-            qh = qs.record(q)[0]
+            qh = qs.header(q)
             sc = scores[q]
             order = np.lexsort((np.arange(len(sc)), -sc.astype(np.int64)))[:a.top]
             for r, i in enumerate(order):
-                out.write("%d\t%s\t%d\t%d\t%d\t%s\n" % (q, qh, r + 1, int(sc[i]), int(i), db.record(int(i))[0]))
+                out.write("%d\t%s\t%d\t%d\t%d\t%s\n" % (q, qh, r + 1, int(sc[i]), int(i), db.header(int(i))))
         print("%d queries x %d records: %.3e cells in %.3f s = %.2f GCUPS"
               % (len(qs), len(db), cells, dt, cells / max(dt, 1e-12) / 1e9), file=sys.stderr)
     return 0

@@ -148,12 +148,16 @@ sw_db* parse_binary(const std::vector<char>& b) {
             return fail(db);
         hsum += (uint64_t)hl[k];
     }
-    if (hsum != hbytes || p + hbytes + nres != b.size()) return fail(db);
+    // sizes compared without sums that could wrap: the headers and then exactly
+    // nres residue bytes must fill the rest of the file
+    if (hsum != hbytes || p > b.size() || hbytes > b.size() - p || nres != b.size() - p - hbytes) return fail(db);
     db->header.resize((size_t)count);
     for (uint64_t k = 0; k < count; ++k) {
+        if ((size_t)hl[k] > b.size() - p) return fail(db);
         db->header[k].assign(b.data() + p, (size_t)hl[k]);
         p += (size_t)hl[k];
     }
+    if (b.size() - p != nres) return fail(db);
     db->res.assign(b.begin() + (ptrdiff_t)p, b.end());
     finish(db);
     return db;
@@ -170,7 +174,9 @@ sw_db* parse_binary(const std::vector<char>& b) {
         }                                                                                    \
     } while (0)
 
-// the database's device arena on the current device, with room for a query of qlen
+// the database's device arena on the current device, with room for a query of qlen.
+// A new arena is built in locals and committed to the Dev entry only when every
+// step succeeded (a failed copy must not leave an arena that looks ready).
 int device_arena(sw_db* db, int qlen, sw_db::Dev** out) {
     int d = 0;
     DBCHK(hipGetDevice(&d));
@@ -180,20 +186,48 @@ int device_arena(sw_db* db, int qlen, sw_db::Dev** out) {
         if (v.scores) DBCHK(hipFree(v.scores));
         v.arena = nullptr;
         v.scores = nullptr;
-        v.qcap = std::max<size_t>((size_t)qlen + (size_t)qlen / 4, 4096);
-        DBCHK(hipMalloc((void**)&v.arena, db->res.size() + v.qcap));
-        DBCHK(hipMalloc((void**)&v.scores, std::max<size_t>(db->len.size(), 1) * sizeof(int)));
-        if (!db->res.empty()) DBCHK(hipMemcpy(v.arena, db->res.data(), db->res.size(), hipMemcpyHostToDevice));
+        v.qcap = 0;
+        const size_t qcap = std::max<size_t>((size_t)qlen + (size_t)qlen / 4, 4096);
+        unsigned char* arena = nullptr;
+        int* scores = nullptr;
+        hipError_t e = hipMalloc((void**)&arena, db->res.size() + qcap);
+        if (e == hipSuccess) e = hipMalloc((void**)&scores, std::max<size_t>(db->len.size(), 1) * sizeof(int));
+        if (e == hipSuccess && !db->res.empty())
+            e = hipMemcpy(arena, db->res.data(), db->res.size(), hipMemcpyHostToDevice);
+        if (e != hipSuccess) {
+            if (arena) (void)hipFree(arena);
+            if (scores) (void)hipFree(scores);
+            char m[256];
+            std::snprintf(m, sizeof m, "database device arena: %s", hipGetErrorString(e));
+            report_error(m);
+            return -1;
+        }
+        v.arena = arena;
+        v.scores = scores;
+        v.qcap = qcap;
     }
     *out = &v;
     return 0;
 }
 
-int search(sw_db* db, const unsigned char* query, int qlen, int* scores_out) {
+// qslot: room to reserve for the query (>= qlen; a query database sizes it once
+// for its longest query, so the residue arena is uploaded once)
+int search(sw_db* db, const unsigned char* query, int qlen, int* scores_out, int qslot) {
     const int nrec = (int)db->len.size();
     if (nrec == 0) return 0;
+    // the engine's int32 score range, checked here so an error names the record
+    int match = 1;
+    sw_get_params(&match, nullptr, nullptr, nullptr);
+    for (int r = 0; r < nrec; ++r) {
+        if ((long long)std::min(qlen, db->len[r]) * std::max(match, 1) >= (1LL << 28)) {
+            char m[160];
+            std::snprintf(m, sizeof m, "record %d: score range exceeds the int32 engine (min length * MATCH >= 2^28)", r);
+            report_error(m);
+            return -1;
+        }
+    }
     sw_db::Dev* v = nullptr;
-    if (device_arena(db, qlen, &v)) return -1;
+    if (device_arena(db, std::max(qlen, qslot), &v)) return -1;
     const int64_t qoff = (int64_t)db->res.size();
     if (qlen > 0) DBCHK(hipMemcpy(v->arena + qoff, query, (size_t)qlen, hipMemcpyHostToDevice));
     std::vector<int64_t> a_off((size_t)nrec, qoff), b_off((size_t)nrec);
@@ -286,7 +320,7 @@ int sw_db_search(sw_db* db, const unsigned char* query, int qlen, int* scores_ou
         return -1;
     }
     std::lock_guard<std::mutex> g(db->mu);
-    return search(db, query, qlen, scores_out);
+    return search(db, query, qlen, scores_out, qlen);
 }
 
 int sw_db_search_db(sw_db* db, const sw_db* queries, int* scores_out) {
@@ -296,8 +330,11 @@ int sw_db_search_db(sw_db* db, const sw_db* queries, int* scores_out) {
     }
     std::lock_guard<std::mutex> g(db->mu);
     const size_t nrec = db->len.size();
+    int longest = 0;
+    for (int l : queries->len) longest = std::max(longest, l);
     for (size_t q = 0; q < queries->len.size(); ++q)
-        if (search(db, queries->res.data() + queries->off[q], queries->len[q], scores_out + q * nrec)) return -1;
+        if (search(db, queries->res.data() + queries->off[q], queries->len[q], scores_out + q * nrec, longest))
+            return -1;
     return 0;
 }
 

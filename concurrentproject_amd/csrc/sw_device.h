@@ -4,6 +4,8 @@
 #pragma once
 #include "sw_internal.h"
 
+#include <type_traits>
+
 namespace swmi {
 namespace {
 
@@ -71,39 +73,91 @@ __device__ __forceinline__ int find_pair(const KParams& kp, int item) {
     return __builtin_amdgcn_readfirstlane(lo);
 }
 
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t bnd_rsrc(const KParams& kp, const PairDesc& pd, int boundary) {
+// ---- strip / group edges ----------------------------------------------------
+// An edge carries one column's (H - G_INIT, E - G_EXT) per row from a producer
+// strip to its consumer as tagged 16-B granules.  Row r of the edge lives at
+// stream position pos0 + r, in slot (pos0 + r) & mask of the edge's buffer, and
+// its checksum covers the position (granule_chk), so a slot still holding an
+// older position -- or an older launch's epoch -- never passes the check:
+//   * linear edges (one m-row buffer per boundary, write-once): pos0 = 0, mask = ~0;
+//   * ring edges (flow2 ring mode, sw_flow2.hip): a boundary's rows stream through a
+//     power-of-two ring shared by every round of one block, pos0 = round * m;
+//   * slab edges (another GPU's kernel writes them over xGMI): linear, and every
+//     load and store of them is system scope (sc0 sc1, AUX_SYS) -- the LLVM AMDGPU
+//     memory model's encoding of a relaxed system-scope atomic on gfx942/gfx950,
+//     which keeps the access coherent with a peer agent's stores to this memory
+//     (fine-grained allocation, sw_slab_alloc).  In-GPU edges stay device scope (sc1).
+// The cache policy is a template argument (AUX_SC1 or AUX_SYS), fixed per
+// instantiation of a kernel's hand-off loop: a runtime choice would put each load
+// and store behind a branch, and the compiler's vmcnt counting across such joins
+// falls back to full drains, which costs the prefetch distance (measured: C2
+// 4.9 -> 6.9 ms).
+struct Edge {
+    __amdgpu_buffer_rsrc_t rsrc;
+    unsigned pos0;    // stream position of row 0
+    unsigned mask;    // slot = (pos0 + row) & mask
+    unsigned epoch;   // tag of this launch's granules
+};
+constexpr int AUX_SYS = 17;   // cache policy sc0|sc1: system scope
+
+__device__ __forceinline__ unsigned edge_off(const Edge& e, int row) { return ((e.pos0 + (unsigned)row) & e.mask) * 16u; }
+
+// the granule of row `row` (store with offset OOR where `st` is false: dropped)
+template <int AUX = AUX_SC1>
+__device__ __forceinline__ void edge_publish(const Edge& e, int row, bool st, int hg, int eh) {
+    u32x4 g;
+    g.x = e.epoch;
+    g.y = (unsigned)hg;
+    g.z = (unsigned)eh;
+    g.w = granule_chk(e.epoch, hg, eh, (int)(e.pos0 + (unsigned)row));
+    __builtin_amdgcn_raw_buffer_store_b128(g, e.rsrc, st ? edge_off(e, row) : OOR, 0, AUX);
+}
+
+// Rows up to 2^27 - 1 (the host rejects longer ones): m * 16 fits the 32-bit record count.
+__device__ __forceinline__ Edge linear_edge(Granule* base, int m, unsigned epoch) {
+    return Edge{__builtin_amdgcn_make_buffer_rsrc(base, 0, (int)((unsigned)m * 16u), RSRC_FLAGS), 0u, ~0u, epoch};
+}
+
+// strip / pairwg kernels: the buffer of strip boundary `boundary` of a pair
+__device__ __forceinline__ Edge strip_edge(const KParams& kp, const PairDesc& pd, int boundary) {
     Granule* base = kp.bnd + pd.bnd_off + (uint64_t)(boundary < 0 ? 0 : boundary) * (uint64_t)pd.m;
-    return __builtin_amdgcn_make_buffer_rsrc(base, 0, pd.m * 16, RSRC_FLAGS);
+    return linear_edge(base, pd.m, kp.epoch);
 }
 
-// Grouped modes: granule buffer of group boundary b (between groups b and b+1).
+// Grouped modes: the edge of group boundary b (between groups b and b+1).
 // b = -1 is the slab inflow and b = ngroups-1 the slab outflow of a multi-GPU
-// column slab (KParams::slab_in / slab_out); without a slab those roles never
-// reach a granule load or store, and the resource points at the arena.
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t group_rsrc(const KParams& kp, const PairDesc& pd, int b,
-                                                             int ngroups) {
-    Granule* base = kp.bnd + pd.bnd_off + (uint64_t)(b < 0 ? 0 : b) * (uint64_t)pd.m;
-    if (b < 0 && kp.slab_in != nullptr) base = kp.slab_in;
-    if (b >= ngroups - 1 && kp.slab_out != nullptr) base = kp.slab_out;
-    return __builtin_amdgcn_make_buffer_rsrc(base, 0, pd.m * 16, RSRC_FLAGS);
-}
-// epoch of the granules crossing group boundary b (slab edges carry the ranks' common epoch)
-__device__ __forceinline__ unsigned group_epoch(const KParams& kp, int b, int ngroups) {
-    if (b < 0 && kp.slab_in != nullptr) return kp.slab_epoch;
-    if (b >= ngroups - 1 && kp.slab_out != nullptr) return kp.slab_epoch;
-    return kp.epoch;
+// column slab (KParams::slab_in / slab_out, the ranks' common epoch); without a
+// slab those roles never reach a granule load or store.  In ring mode
+// (kp.ring_rows > 0, one pair, block j runs groups j, j + G, j + 2G, ... for a
+// grid of G blocks) boundary b = k*G + j goes through ring j when j < G - 1
+// (both groups run in round k) and through the wrap ring otherwise (the
+// consumer, block 0, runs it in round k + 1).
+__device__ __forceinline__ Edge group_edge(const KParams& kp, const PairDesc& pd, int b, int ngroups) {
+    if (b < 0 && kp.slab_in != nullptr) return linear_edge(kp.slab_in, pd.m, kp.slab_epoch);
+    if (b >= ngroups - 1 && kp.slab_out != nullptr) return linear_edge(kp.slab_out, pd.m, kp.slab_epoch);
+    const int bb = b < 0 ? 0 : b;
+    if (kp.ring_rows > 0) {
+        const int G = (int)gridDim.x;
+        const int j = bb % G, k = bb / G;
+        const bool wrap = j == G - 1;
+        const int rows = wrap ? kp.wrap_rows : kp.ring_rows;
+        Granule* base = kp.bnd + (uint64_t)j * (uint64_t)kp.ring_rows;
+        return Edge{__builtin_amdgcn_make_buffer_rsrc(base, 0, rows * 16, RSRC_FLAGS), (unsigned)k * (unsigned)pd.m,
+                    (unsigned)rows - 1u, kp.epoch};
+    }
+    return linear_edge(kp.bnd + pd.bnd_off + (uint64_t)bb * (uint64_t)pd.m, pd.m, kp.epoch);
 }
 
-__device__ __forceinline__ bool granule_ok(const u32x4& g, unsigned epoch, int row) {
+__device__ __forceinline__ bool granule_ok(const u32x4& g, const Edge& e, int row) {
     // bitwise, not short-circuit: no exec-mask branch per lane
-    return (g.x == epoch) & (g.w == granule_chk(epoch, (int)g.y, (int)g.z, row));
+    return (g.x == e.epoch) & (g.w == granule_chk(e.epoch, (int)g.y, (int)g.z, (int)(e.pos0 + (unsigned)row)));
 }
 
-template <int C>
-__device__ __forceinline__ u32x4 fetch_granules(const __amdgpu_buffer_rsrc_t in_rsrc, int k0, int lane, int m) {
+template <int C, int AUX = AUX_SC1>
+__device__ __forceinline__ u32x4 fetch_granules(const Edge& e, int k0, int lane, int m) {
     const int row = k0 + lane;
     const bool live = lane < C && row >= 0 && row < m;
-    return __builtin_amdgcn_raw_buffer_load_b128(in_rsrc, live ? (unsigned)row * 16u : OOR, 0, AUX_SC1);
+    return __builtin_amdgcn_raw_buffer_load_b128(e.rsrc, live ? edge_off(e, row) : OOR, 0, AUX);
 }
 
 // Slow path of await_granules: re-poll until every granule of the chunk is
@@ -115,15 +169,21 @@ struct AwaitRes {
     u32x4 g;
     int failed;
 };
-__device__ __noinline__ AwaitRes await_slow(__amdgpu_buffer_rsrc_t in_rsrc, u32x4 g, const int row, const bool need,
-                                            const unsigned epoch, const long long timeout_ticks, Ctrl* ctrl,
-                                            const int strip, const int lane) {
+// (The edge goes in as its parts, not as an Edge: a struct argument of a call
+// made the compiler keep the caller's buffer resource in VGPRs across the call
+// and wrap every granule load of the chunk loop in a waterfall loop.)
+template <int AUX>
+__device__ __noinline__ AwaitRes await_slow(__amdgpu_buffer_rsrc_t rsrc, unsigned pos0, unsigned mask,
+                                            unsigned epoch, u32x4 g, const int row, const bool need,
+                                            const long long timeout_ticks, Ctrl* ctrl, const int strip,
+                                            const int lane) {
+    const Edge e{rsrc, pos0, mask, epoch};
     const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
-    bool ok = !need || granule_ok(g, epoch, row);
+    bool ok = !need || granule_ok(g, e, row);
     for (;;) {
         __builtin_amdgcn_s_sleep(1);
-        if (!ok) g = __builtin_amdgcn_raw_buffer_load_b128(in_rsrc, (unsigned)row * 16u, 0, AUX_SC1);
-        ok = !need || granule_ok(g, epoch, row);
+        if (!ok) g = __builtin_amdgcn_raw_buffer_load_b128(e.rsrc, edge_off(e, row), 0, AUX);
+        ok = !need || granule_ok(g, e, row);
         if (__all(ok)) return AwaitRes{g, 0};
         if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > timeout_ticks) {
             if (lane == 0) {
@@ -135,16 +195,17 @@ __device__ __noinline__ AwaitRes await_slow(__amdgpu_buffer_rsrc_t in_rsrc, u32x
     }
 }
 
-// Wait until the granules of rows [k0, k0+C) are all published with `epoch` (bounded spin).
-template <int C>
-__device__ __forceinline__ void await_granules(const KParams& kp, const __amdgpu_buffer_rsrc_t in_rsrc, u32x4& g,
-                                               int k0, int lane, int m, int strip, bool& failed, unsigned epoch) {
+// Wait until the granules of rows [k0, k0+C) of edge e are all published (bounded spin).
+template <int C, int AUX = AUX_SC1>
+__device__ __forceinline__ void await_granules(const KParams& kp, const Edge& e, u32x4& g, int k0, int lane, int m,
+                                               int strip, bool& failed) {
     if (failed) return;
     const int row = k0 + lane;
     const bool need = lane < C && row >= 0 && row < m;
-    const bool ok = (!need) | granule_ok(g, epoch, row);
+    const bool ok = (!need) | granule_ok(g, e, row);
     if (__all(ok)) return;
-    const AwaitRes r = await_slow(in_rsrc, g, row, need, epoch, kp.timeout_ticks, kp.ctrl, strip, lane);
+    const AwaitRes r = await_slow<AUX>(e.rsrc, e.pos0, e.mask, e.epoch, g, row, need, kp.timeout_ticks, kp.ctrl,
+                                       strip, lane);
     g = r.g;
     failed = r.failed != 0;
 }
@@ -155,7 +216,31 @@ __device__ __forceinline__ int lds_load(const int* p) {
 __device__ __forceinline__ void compiler_fence() { __asm__ __volatile__("" ::: "memory"); }
 
 // where a wave's strip inflow comes from / its outflow goes (flow kernels)
-enum : int { FLOW_NONE = 0, FLOW_GRANULE = 1, FLOW_LDS = 2 };
+// (FLOW_PEER: a slab edge, granules to / from another GPU, system scope)
+enum : int { FLOW_NONE = 0, FLOW_GRANULE = 1, FLOW_LDS = 2, FLOW_PEER = 3 };
+// the cache policy of a granule hand-off kind
+__host__ __device__ constexpr int flow_aux(int kind) { return kind == FLOW_PEER ? AUX_SYS : AUX_SC1; }
+__host__ __device__ constexpr bool flow_granule(int kind) { return kind == FLOW_GRANULE || kind == FLOW_PEER; }
+
+// A strip's (inflow, outflow) kinds as compile-time constants: calls f(IN{}, OUT{}),
+// so every hand-off loop is instantiated per role with unconditional memory ops.
+template <class F>
+__device__ __forceinline__ void dispatch_kinds(int in_kind, int out_kind, F&& f) {
+    using K0 = std::integral_constant<int, FLOW_NONE>;
+    using K1 = std::integral_constant<int, FLOW_GRANULE>;
+    using K2 = std::integral_constant<int, FLOW_LDS>;
+    using K3 = std::integral_constant<int, FLOW_PEER>;
+    auto outs = [&](auto in_c) __attribute__((always_inline)) {
+        if (out_kind == FLOW_LDS) f(in_c, K2{});
+        else if (out_kind == FLOW_GRANULE) f(in_c, K1{});
+        else if (out_kind == FLOW_PEER) f(in_c, K3{});
+        else f(in_c, K0{});
+    };
+    if (in_kind == FLOW_LDS) outs(K2{});
+    else if (in_kind == FLOW_GRANULE) outs(K1{});
+    else if (in_kind == FLOW_PEER) outs(K3{});
+    else outs(K0{});
+}
 
 #ifndef SW_SPIN_SLEEP
 #define SW_SPIN_SLEEP 1      // s_sleep units (64 cycles) between LDS progress polls

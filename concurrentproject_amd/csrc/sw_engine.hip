@@ -21,6 +21,7 @@
 #include <cstring>
 #include <map>
 #include <mutex>
+#include <set>
 #include <string>
 #include <vector>
 
@@ -56,7 +57,13 @@ std::mutex g_param_mu;
 Params g_params;
 
 std::atomic<long long> g_opt_W{0}, g_opt_C{0}, g_opt_bytes{0}, g_opt_timeout{30}, g_opt_blocks{0}, g_opt_orient{0},
-    g_opt_mode{-1}, g_opt_trace{0}, g_opt_duo_f16{1}, g_opt_f2stream{0};
+    g_opt_mode{-1}, g_opt_trace{0}, g_opt_duo_f16{1}, g_opt_f2stream{0}, g_opt_ring{-1}, g_opt_ring_rows{4096};
+
+// Longest sequence the engine takes: granule buffers of m rows keep m * 16 in the
+// 32-bit record count of a buffer resource (sw_device.h linear_edge).
+constexpr long long MAX_SEQ = (1LL << 27) - 1;
+// flow2 ring mode (auto): when one-buffer-per-boundary edges would exceed this
+constexpr long long RING_AUTO_BYTES = 1LL << 30;
 
 // orientation: 0 = engine policy, 1 = seq1 across lanes (columns), 2 = seq2 across lanes
 bool want_swap(bool single, long long len1, long long len2) {
@@ -128,6 +135,7 @@ struct Ctx {
     DevBuf<Ctrl> ctrl;
     DevBuf<int> scores;
     DevBuf<unsigned> flag;
+    DevBuf<unsigned> cons;            // flow2 ring mode: consumer progress words
     DevBuf<DuoDesc> duo;
     PinBuf<DuoDesc> hduo;
     PinBuf<unsigned char> hseq;
@@ -183,6 +191,7 @@ struct Job {
     std::vector<DuoDesc> duos;   // MODE_DUO only
     bool duo_f16 = false;        // MODE_DUO: max3 through v_pk_maximum3_f16 (duo_f16_fits)
     bool f2_stream = false;      // MODE_FLOW2: row codes streamed (rows too long to stage in LDS)
+    bool ring = false;           // MODE_FLOW2, one pair: group edges through per-block rings (O(m) state)
 };
 
 bool is_dna_byte(unsigned char c) { return c == 'A' || c == 'C' || c == 'G' || c == 'T'; }
@@ -338,6 +347,18 @@ void plan_flow2(Job& job) {
         job.item_base[k + 1] = job.item_base[k] + (d.strips + 3) / 4;
     }
     job.bnd_granules = g;
+    // Ring mode (sw_flow2.hip, KParams::ring_rows): one pair whose write-once group
+    // edges would take more than RING_AUTO_BYTES (C5: 69.8 GB), or when forced.  Stream
+    // positions are 32-bit and may wrap: slots are taken mod a power of two <= 2^24,
+    // progress words are compared as serial numbers, and a slot's previous position
+    // differs from the current one by the ring size (< 2^25), which the checksum's
+    // 25 position bits always see.  Hence rows <= 2^24.
+    const long long opt = g_opt_ring.load();
+    if (job.pairs.size() == 1 && opt != 0 && job.item_base[1] > 1) {
+        const PairDesc& d = job.pairs[0];
+        const bool ok = d.m <= (1 << 24);
+        job.ring = ok && (opt == 1 || (long long)(g * sizeof(Granule)) > RING_AUTO_BYTES);
+    }
 }
 
 int finalize_mode(Job& job, const Params& prm) {
@@ -355,7 +376,7 @@ int finalize_mode(Job& job, const Params& prm) {
     if (job.mode == MODE_FLOW2 || (g_opt_mode.load() < 0 && job.mode == MODE_CHAIN)) {
         if (flow2_fits(job, prm)) {
             plan_flow2(job);
-            job.f2_stream = !flow2_staged(job, max_m);
+            job.f2_stream = job.ring || !flow2_staged(job, max_m);   // ring mode runs with streamed codes
             return 0;
         }
         if (job.mode == MODE_FLOW2) {
@@ -484,6 +505,17 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
     // a fresh control block holds whatever the allocator recycled: clear the sticky
     // error fields once (afterwards only check_ctrl resets them, after reporting)
     if (c->ctrl.p != ctrl_before) HIPCHK(hipMemsetAsync(c->ctrl.p, 0, sizeof(Ctrl), s));
+    // ring mode: every block resident (one workgroup per CU for flow2), rings sized by the grid
+    int ring_blocks = 0, wrap_rows = 0;
+    if (job.ring) {
+        ring_blocks = std::min(job.item_base[np], c->cus);
+        if (g_opt_blocks.load() > 0) ring_blocks = (int)std::min<long long>(g_opt_blocks.load(), job.item_base[np]);
+        wrap_rows = 1;
+        while (wrap_rows < job.pairs[0].m) wrap_rows *= 2;
+        job.bnd_granules = (uint64_t)(ring_blocks - 1) * (uint64_t)g_opt_ring_rows.load() + (uint64_t)wrap_rows;
+        if (c->cons.ensure((size_t)ring_blocks * RING_CONS_STRIDE, s)) return -1;
+        HIPCHK(hipMemsetAsync(c->cons.p, 0, (size_t)ring_blocks * RING_CONS_STRIDE * sizeof(unsigned), s));
+    }
     if (job.bnd_granules) {
         size_t freeb = 0, totb = 0;
         HIPCHK(hipMemGetInfo(&freeb, &totb));
@@ -521,6 +553,15 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
         // the CU count would only park extra workgroups until a CU frees up
         if (job.mode == MODE_FLOW2) blocks = std::min<long long>(blocks, c->cus);
     }
+    if (job.ring) {
+        // the static item deal needs every block resident at once; flow2 pads its LDS to
+        // more than half a CU's, so one workgroup per CU
+        if (ring_blocks > c->cus) {
+            set_err("flow2 ring mode needs all %d workgroups co-resident (one per CU, %d CUs)", ring_blocks, c->cus);
+            return -1;
+        }
+        blocks = ring_blocks;
+    }
     cfg.blocks = (int)std::max<long long>(1, blocks);
 
     KParams kp{};
@@ -552,6 +593,11 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
     }
     kp.timeout_ticks = g_opt_timeout.load() * 100000000LL;   // s_memrealtime: 100 MHz
     kp.trace = reinterpret_cast<unsigned long long*>(g_opt_trace.load());
+    if (job.ring) {
+        kp.ring_rows = (int)g_opt_ring_rows.load();
+        kp.wrap_rows = wrap_rows;
+        kp.ring_cons = c->cons.p;
+    }
     if (edge) {
         kp.slab_in = edge->in;
         kp.slab_out = edge->out;
@@ -571,7 +617,7 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
     t_stats.waves_per_cu = wpc;
     t_stats.items = items;
     t_stats.mode = job.mode;
-    t_stats.variant = (cfg.duo_f16 ? 1 : 0) | (cfg.f2_stream ? 2 : 0);
+    t_stats.variant = (cfg.duo_f16 ? 1 : 0) | (cfg.f2_stream ? 2 : 0) | (job.ring ? 4 : 0);
     t_stats.boundary_bytes = (long long)(job.bnd_granules * sizeof(Granule));
     c->last = s;
     return 0;
@@ -613,6 +659,10 @@ int score_host(const HostPair* in, int npairs, const Params& prm, int* out) {
         }
         if ((long long)std::min(in[k].n, in[k].m) * std::max(prm.match, 1) >= (1LL << 28)) {
             set_err("pair %d: score range exceeds the int32 engine (min length * MATCH >= 2^28)", k);
+            return -1;
+        }
+        if (in[k].n > MAX_SEQ || in[k].m > MAX_SEQ) {
+            set_err("pair %d: sequences longer than 2^27 - 1 bytes are not supported", k);
             return -1;
         }
         out[k] = 0;   // empty pairs score 0 (main.cpp:74-90 with empty loops)
@@ -708,6 +758,19 @@ __global__ void alphabet_kernel(const unsigned char* arena, const PairDesc* pair
 // the thread's sw_last_error() text, for the other host modules (sw_db.hip)
 void report_error(const char* msg) { set_err("%s", msg); }
 
+hipError_t raise_dyn_lds(const void* fn, int bytes) {
+    static std::mutex mu;
+    static std::set<std::pair<const void*, int>> done;
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    std::lock_guard<std::mutex> g(mu);
+    if (done.count({fn, dev})) return hipSuccess;
+    e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+    if (e == hipSuccess) done.insert({fn, dev});
+    return e;
+}
+
 }  // namespace swmi
 
 using namespace swmi;
@@ -795,6 +858,10 @@ int sw_score_batch_device(const unsigned char* d_arena, const int64_t* a_off, co
         }
         if ((long long)std::min(alen[k], blen[k]) * std::max(prm.match, 1) >= (1LL << 28)) {
             set_err("pair %d: score range exceeds the int32 engine", k);
+            return -1;
+        }
+        if (alen[k] > MAX_SEQ || blen[k] > MAX_SEQ) {
+            set_err("pair %d: sequences longer than 2^27 - 1 bytes are not supported", k);
             return -1;
         }
         if (alen[k] > 0 && blen[k] > 0) idx.push_back(k);
@@ -890,6 +957,10 @@ int sw_score_slab_device(const unsigned char* d_arena, int64_t col_off, int n, i
     // H of any cell is at most MATCH * (its row), whatever the slab's column range
     if ((long long)m * std::max(prm.match, 1) >= (1LL << 28)) {
         set_err("slab: rows * MATCH >= 2^28 exceeds the int32 engine");
+        return -1;
+    }
+    if (m > MAX_SEQ) {
+        set_err("slab: more than 2^27 - 1 rows are not supported");
         return -1;
     }
     Ctx* c = get_ctx();
@@ -1016,6 +1087,12 @@ int sw_set_option(const char* key, long long v) {
         g_opt_duo_f16 = v ? 1 : 0;
     } else if (k == "f2stream") {   // 1 = flow2 streams row codes even when they fit in LDS (tests)
         g_opt_f2stream = v ? 1 : 0;
+    } else if (k == "ring") {   // flow2 one-pair group edges: -1 auto (rings above 1 GB of edges), 0 off, 1 on
+        if (v < -1 || v > 1) return -1;
+        g_opt_ring = v;
+    } else if (k == "ring_rows") {   // rows per within-round ring: a power of two in [512, 2^20]
+        if (v < 512 || v > (1 << 20) || (v & (v - 1))) return -1;
+        g_opt_ring_rows = v;
     } else {
         set_err("unknown option '%s'", key);
         return -1;
@@ -1036,6 +1113,8 @@ long long sw_get_option(const char* key) {
     if (k == "mode") return g_opt_mode;
     if (k == "duo16") return g_opt_duo_f16;
     if (k == "f2stream") return g_opt_f2stream;
+    if (k == "ring") return g_opt_ring;
+    if (k == "ring_rows") return g_opt_ring_rows;
     return -1;
 }
 

@@ -96,8 +96,11 @@ __device__ __forceinline__ int sbyte(unsigned w) {
 // store the codes of chunk c+2 (two ds_write_b8).  The step loop is unchanged.
 constexpr int F2_CR = 256;
 
-template <int C, bool STREAM>
+// RING: ring-mode edges (KParams::ring_rows > 0; streamed codes only).  A separate
+// instantiation, so the linear-edge kernel carries none of its back-pressure code.
+template <int C, bool STREAM, bool RING>
 __global__ void __launch_bounds__(256) sw_flow2_kernel(KParams kp) {
+    static_assert(!RING || STREAM, "ring mode runs the streamed-codes kernel");
     static_assert(C % 4 == 0 && 64 % C == 0 && 2 * C + 64 <= F2_R, "chunk");
     // STREAM ring: during chunk c the reads span rows [k0 + C - 63, k0 + 2C) and the
     // writes rows [k0 + 2C, k0 + 3C): no slot is rewritten while still read
@@ -114,8 +117,10 @@ __global__ void __launch_bounds__(256) sw_flow2_kernel(KParams kp) {
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane((int)(tid >> 6));
     const int go = kp.gap_init, ge = kp.gap_ext;
-    for (;;) {
-        if (tid == 0) s_item = (int)atomicAdd(&kp.ctrl->next_item, 1u);
+    for (int it = 0;; ++it) {
+        // items are claimed in order (any grid size), or in ring mode dealt statically:
+        // block j runs items j, j + G, j + 2G, ... (every block resident, see group_edge)
+        if (tid == 0) s_item = RING ? (int)blockIdx.x + it * (int)gridDim.x : (int)atomicAdd(&kp.ctrl->next_item, 1u);
         __syncthreads();   // every wave is done with the previous item
         const int item = __builtin_amdgcn_readfirstlane(s_item);
         if (item >= kp.total_items) return;
@@ -150,13 +155,27 @@ __global__ void __launch_bounds__(256) sw_flow2_kernel(KParams kp) {
         // a multi-GPU column slab: the first strip takes the previous slab's edge, the
         // last one hands its lane-62 column (the next slab's left neighbour) on
         const int ngroups = (pd.strips + 3) / 4;
-        const int in_kind = wave > 0 ? FLOW_LDS : (strip > 0 || kp.slab_in != nullptr) ? FLOW_GRANULE : FLOW_NONE;
-        const int out_kind = strip + 1 >= pd.strips ? (kp.slab_out != nullptr ? FLOW_GRANULE : FLOW_NONE)
+        const int in_kind = wave > 0 ? FLOW_LDS : strip > 0 ? FLOW_GRANULE : kp.slab_in != nullptr ? FLOW_PEER : FLOW_NONE;
+        const int out_kind = strip + 1 >= pd.strips ? (kp.slab_out != nullptr ? FLOW_PEER : FLOW_NONE)
                              : wave < 3           ? FLOW_LDS
                                                   : FLOW_GRANULE;
-        const __amdgpu_buffer_rsrc_t in_rsrc = group_rsrc(kp, pd, group - 1, ngroups);
-        const __amdgpu_buffer_rsrc_t out_rsrc = group_rsrc(kp, pd, group, ngroups);
-        const unsigned ep_in = group_epoch(kp, group - 1, ngroups), ep_out = group_epoch(kp, group, ngroups);
+        const Edge in_e = group_edge(kp, pd, group - 1, ngroups);
+        const Edge out_e = group_edge(kp, pd, group, ngroups);
+        // ring mode: the consumer of ring j reports the positions it has consumed in
+        // ring_cons[j]; the producer never overwrites a slot whose position is not
+        // consumed yet (back-pressure).  The wrap ring holds >= m rows and needs none:
+        // its consumer (block 0, round k+1) has read row r of round k before the chain
+        // of round k+1 lets block G-1 produce row r again.
+        unsigned* cons_in = nullptr;
+        unsigned* bp_word = nullptr;
+        if constexpr (RING) {
+            const int G = (int)gridDim.x;
+            if (group > 0 && (group - 1) % G != G - 1) cons_in = kp.ring_cons + ((group - 1) % G) * RING_CONS_STRIDE;
+            if (group < ngroups - 1 && group % G != G - 1) bp_word = kp.ring_cons + (group % G) * RING_CONS_STRIDE;
+        }
+        const bool cons_live = cons_in != nullptr;
+        const __amdgpu_buffer_rsrc_t cons_rsrc = __builtin_amdgcn_make_buffer_rsrc(cons_live ? cons_in : nullptr, 0,
+                                                                                    cons_live ? 4 : 0, RSRC_FLAGS);
         const long long t_start = (long long)__builtin_amdgcn_s_memrealtime();
         bool failed = false;
         long long t_first = t_start;
@@ -208,11 +227,12 @@ __global__ void __launch_bounds__(256) sw_flow2_kernel(KParams kp) {
 
         auto flow_loop = [&](auto in_c, auto out_c) __attribute__((always_inline)) {
             constexpr int IN = decltype(in_c)::value, OUT = decltype(out_c)::value;
+            constexpr int AIN = flow_aux(IN), AOUT = flow_aux(OUT);
             // granule prefetch queue: gq[i] holds the loads for chunk c + i (issued SW_F2_GPREF chunks ahead)
             u32x4 gq[SW_F2_GPREF];
 #pragma unroll
             for (int i = 0; i < SW_F2_GPREF; ++i)
-                gq[i] = IN == FLOW_GRANULE ? fetch_granules<C>(in_rsrc, i * C, lane, m) : u32x4{0u, 0u, 0u, 0u};
+                gq[i] = flow_granule(IN) ? fetch_granules<C, AIN>(in_e, i * C, lane, m) : u32x4{0u, 0u, 0u, 0u};
             unsigned D[C / 4];
 #pragma unroll
             for (int u = 0; u < C / 4; ++u) D[u] = load_u32_unaligned(code_at(0) + 4 * u);
@@ -222,16 +242,29 @@ __global__ void __launch_bounds__(256) sw_flow2_kernel(KParams kp) {
             // granule outflow at step k0 (chunk start, or mid-chunk with SW_F2_HALFPUB):
             // lane L >= 64 - C holds row k0 - 128 + L; with half-chunk publishing only
             // lanes >= 64 - C/2 are new
+            unsigned bp_seen = 0;   // ring mode: last value read of the consumer's progress word
             auto publish_granules_half = [&](const int k0) __attribute__((always_inline)) {
                 const int row_out = k0 - 128 + lane;
                 constexpr int LO = SW_F2_HALFPUB ? 64 - C / 2 : 64 - C;
                 const bool st = lane >= LO && row_out >= 0 && row_out < m;
-                u32x4 g;
-                g.x = ep_out;
-                g.y = (unsigned)IOH;
-                g.z = (unsigned)IOE;
-                g.w = granule_chk(ep_out, IOH, IOE, row_out);
-                __builtin_amdgcn_raw_buffer_store_b128(g, out_rsrc, st ? (unsigned)row_out * 16u : OOR, 0, AUX_SC1);
+                if (RING && bp_word != nullptr && k0 - 64 > kp.ring_rows) {
+                    // rows <= k0 - 65 go out: positions <= pos0 + k0 - 65 - R must be consumed
+                    const unsigned need = out_e.pos0 + (unsigned)(k0 - 64 - kp.ring_rows);
+                    if ((int)(bp_seen - need) < 0) {
+                        bp_seen = __builtin_amdgcn_readfirstlane(
+                            __hip_atomic_load(bp_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+                        while ((int)(bp_seen - need) < 0) {
+                            __builtin_amdgcn_s_sleep(SW_SPIN_SLEEP);
+                            bp_seen = __builtin_amdgcn_readfirstlane(
+                                __hip_atomic_load(bp_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+                            if ((long long)__builtin_amdgcn_s_memrealtime() - t_start > kp.timeout_ticks) {
+                                failed = true;
+                                break;
+                            }
+                        }
+                    }
+                }
+                edge_publish<AOUT>(out_e, row_out, st, IOH, IOE);
             };
             // ---- publish the last chunk's outflow: lane L >= 64 - C holds row k0 - 128 + L
             auto publish = [&](const int k0) __attribute__((always_inline)) {
@@ -254,7 +287,7 @@ __global__ void __launch_bounds__(256) sw_flow2_kernel(KParams kp) {
                     *dst = make_int2(IOH, IOE);
                     compiler_fence();
                     *prod_out = max(0, k0 - 64);   // after the ring writes (in-order DS)
-                } else if constexpr (OUT == FLOW_GRANULE) {
+                } else if constexpr (flow_granule(OUT)) {
                     publish_granules_half(k0);
                 }
             };
@@ -266,18 +299,25 @@ __global__ void __launch_bounds__(256) sw_flow2_kernel(KParams kp) {
 #endif
                 // ---- inflow rows [k0, k0 + C), for lanes [0, C) of the I/O registers
                 int newH, newE;
-                if constexpr (IN == FLOW_GRANULE) {
+                if constexpr (flow_granule(IN)) {
                     u32x4 g = gq[0];
                     if (kp.trace != nullptr) {   // tools: count chunks whose granules were not there yet
                         const int row = k0 + lane;
                         const bool need = lane < C && row < m;
-                        nslow += __all((!need) | granule_ok(g, ep_in, row)) ? 0 : 1;
+                        nslow += __all((!need) | granule_ok(g, in_e, row)) ? 0 : 1;
                     }
-                    await_granules<C>(kp, in_rsrc, g, k0, lane, m, strip, failed, ep_in);
+                    await_granules<C, AIN>(kp, in_e, g, k0, lane, m, strip, failed);
+                    // ring mode: rows < k0 + C are consumed (reported every 4th chunk and at
+                    // the last).  An unconditional store, dropped (offset OOR) where there is
+                    // nothing to report: no branch around a memory op in the chunk loop.
+                    if constexpr (RING)
+                        __builtin_amdgcn_raw_buffer_store_b32(
+                            in_e.pos0 + (unsigned)min(k0 + C, m), cons_rsrc,
+                            cons_live && lane == 0 && ((c & 3) == 3 || c == nloc - 1) ? 0u : OOR, 0, AUX_SC1);
 #pragma unroll
                     for (int i = 0; i + 1 < SW_F2_GPREF; ++i) gq[i] = gq[i + 1];
                     if constexpr (SW_F2_GPOS == 0)
-                        gq[SW_F2_GPREF - 1] = fetch_granules<C>(in_rsrc, k0 + SW_F2_GPREF * C, lane, m);
+                        gq[SW_F2_GPREF - 1] = fetch_granules<C, AIN>(in_e, k0 + SW_F2_GPREF * C, lane, m);
                     const bool live = k0 + lane < m;
                     newH = live ? (int)g.y : -go;
                     newE = live ? (int)g.z : -ge;
@@ -356,10 +396,10 @@ __global__ void __launch_bounds__(256) sw_flow2_kernel(KParams kp) {
                 // ---- C anti-diagonal steps
 #pragma unroll
                 for (int j = 0; j < C; j += 4) {
-                    if constexpr (IN == FLOW_GRANULE && SW_F2_GPOS > 0) {
-                        if (j == SW_F2_GPOS * C / 4) gq[SW_F2_GPREF - 1] = fetch_granules<C>(in_rsrc, k0 + SW_F2_GPREF * C, lane, m);
+                    if constexpr (flow_granule(IN) && SW_F2_GPOS > 0) {
+                        if (j == SW_F2_GPOS * C / 4) gq[SW_F2_GPREF - 1] = fetch_granules<C, AIN>(in_e, k0 + SW_F2_GPREF * C, lane, m);
                     }
-                    if constexpr (OUT == FLOW_GRANULE && SW_F2_HALFPUB) {
+                    if constexpr (flow_granule(OUT) && SW_F2_HALFPUB) {
                         // lanes [64 - C/2, 64) hold this chunk's first C/2 outflow rows
                         if (j == C / 2) publish_granules_half(k0 + C / 2);
                     }
@@ -399,22 +439,7 @@ __global__ void __launch_bounds__(256) sw_flow2_kernel(KParams kp) {
             }
             publish(nloc * C);
         };
-        using I0 = std::integral_constant<int, FLOW_NONE>;
-        using I1 = std::integral_constant<int, FLOW_GRANULE>;
-        using I2 = std::integral_constant<int, FLOW_LDS>;
-        if (in_kind == FLOW_LDS) {
-            if (out_kind == FLOW_LDS) flow_loop(I2{}, I2{});
-            else if (out_kind == FLOW_GRANULE) flow_loop(I2{}, I1{});
-            else flow_loop(I2{}, I0{});
-        } else if (in_kind == FLOW_GRANULE) {
-            if (out_kind == FLOW_LDS) flow_loop(I1{}, I2{});
-            else if (out_kind == FLOW_GRANULE) flow_loop(I1{}, I1{});   // one-strip group between slab edges
-            else flow_loop(I1{}, I0{});
-        } else {
-            if (out_kind == FLOW_LDS) flow_loop(I0{}, I2{});
-            else if (out_kind == FLOW_GRANULE) flow_loop(I0{}, I1{});   // a one-strip first slab
-            else flow_loop(I0{}, I0{});
-        }
+        dispatch_kinds(in_kind, out_kind, flow_loop);
         if (kp.trace != nullptr && lane == 0) {
             unsigned long long* t = kp.trace + 16ull * (unsigned)strip;
             t[0] = (unsigned long long)t_start;
@@ -434,7 +459,7 @@ __global__ void __launch_bounds__(256) sw_flow2_kernel(KParams kp) {
     }
 }
 
-template <int C, bool STREAM>
+template <int C, bool STREAM, bool RING = false>
 hipError_t launch_c(const LaunchCfg& cfg, const KParams& kp, hipStream_t s) {
     // at least half the CU's LDS: one workgroup per CU, so no strip ever shares a
     // SIMD with another (a co-resident waiting workgroup's polls steal issue slots
@@ -443,21 +468,18 @@ hipError_t launch_c(const LaunchCfg& cfg, const KParams& kp, hipStream_t s) {
     const int dyn = STREAM ? pad : std::max(flow2_stage_bytes(cfg.max_m, C), pad);
     const int lim = flow2_stage_max(C) - (STREAM ? 4 * (F2_CR + C + 64) : 0);
     if (dyn > lim) return hipErrorInvalidValue;
-    static int dyn_set = 0;   // raise the dynamic-LDS limit once per variant
-    if (dyn > 64 * 1024 && dyn_set == 0) {
-        const hipError_t e = hipFuncSetAttribute((const void*)sw_flow2_kernel<C, STREAM>,
-                                                 hipFuncAttributeMaxDynamicSharedMemorySize, lim);
+    if (dyn > 64 * 1024) {   // raise the dynamic-LDS limit (once per variant and device)
+        const hipError_t e = raise_dyn_lds((const void*)sw_flow2_kernel<C, STREAM, RING>, lim);
         if (e != hipSuccess) return e;
-        dyn_set = 1;
     }
-    hipLaunchKernelGGL((sw_flow2_kernel<C, STREAM>), dim3(cfg.blocks), dim3(256), (size_t)dyn, s, kp);
+    hipLaunchKernelGGL((sw_flow2_kernel<C, STREAM, RING>), dim3(cfg.blocks), dim3(256), (size_t)dyn, s, kp);
     return hipGetLastError();
 }
 
 template <int C>
 int waves_c() {
     int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)sw_flow2_kernel<C, false>, 256, 0) != hipSuccess)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)sw_flow2_kernel<C, false, false>, 256, 0) != hipSuccess)
         return 4;
     return nb * 4;
 }
@@ -468,9 +490,15 @@ bool flow2_variant_exists(int C) { return C == 16 || C == 32 || C == 64; }
 
 hipError_t launch_sw_flow2(const LaunchCfg& cfg, const KParams& kp, hipStream_t stream) {
     switch (cfg.C) {
-        case 16: return cfg.f2_stream ? launch_c<16, true>(cfg, kp, stream) : launch_c<16, false>(cfg, kp, stream);
-        case 32: return cfg.f2_stream ? launch_c<32, true>(cfg, kp, stream) : launch_c<32, false>(cfg, kp, stream);
-        case 64: return cfg.f2_stream ? launch_c<64, true>(cfg, kp, stream) : launch_c<64, false>(cfg, kp, stream);
+        case 16: return kp.ring_rows > 0 ? launch_c<16, true, true>(cfg, kp, stream)
+                        : cfg.f2_stream  ? launch_c<16, true>(cfg, kp, stream)
+                                         : launch_c<16, false>(cfg, kp, stream);
+        case 32: return kp.ring_rows > 0 ? launch_c<32, true, true>(cfg, kp, stream)
+                        : cfg.f2_stream  ? launch_c<32, true>(cfg, kp, stream)
+                                         : launch_c<32, false>(cfg, kp, stream);
+        case 64: return kp.ring_rows > 0 ? launch_c<64, true, true>(cfg, kp, stream)
+                        : cfg.f2_stream  ? launch_c<64, true>(cfg, kp, stream)
+                                         : launch_c<64, false>(cfg, kp, stream);
         default: return hipErrorInvalidValue;
     }
 }

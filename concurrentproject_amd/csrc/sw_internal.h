@@ -87,7 +87,17 @@ struct KParams {
     Granule* slab_in;
     Granule* slab_out;
     unsigned slab_epoch;
+    // flow2 ring mode (one pair; sw_flow2.hip): 0 = linear edges (one m-row
+    // granule buffer per group boundary, written once).  Else block j of the
+    // G-block grid runs groups j, j+G, j+2G, ...; boundary k*G+j streams through
+    // ring j (ring_rows rows, j < G-1) or the wrap ring (wrap_rows >= m rows,
+    // j = G-1), so the boundary state is O(G*ring_rows + m), not O(groups*m).
+    int ring_rows;
+    int wrap_rows;
+    unsigned* ring_cons;          // ring j's consumer progress (positions consumed), RING_CONS_STRIDE apart
 };
+
+constexpr int RING_CONS_STRIDE = 32;   // dwords between consumer progress words (one 128-B line each)
 
 // Grid organisations (sw_kernels.hip):
 //   MODE_STRIP  independent waves claim (pair, strip) items in order
@@ -138,6 +148,8 @@ __host__ __device__ constexpr int flow2_static_lds(int C) { return 4 * 256 * 8 +
 __host__ __device__ constexpr int flow2_stage_max(int C) { return LDS_PER_CU - flow2_static_lds(C) - 256; }
 // sets the calling thread's sw_last_error() text (sw_engine.hip)
 void report_error(const char* msg);
+// hipFuncSetAttribute(fn, MaxDynamicSharedMemorySize, bytes) once per (kernel, device) (sw_engine.hip)
+hipError_t raise_dyn_lds(const void* fn, int bytes);
 
 hipError_t launch_sw_flow2(const LaunchCfg& cfg, const KParams& kp, hipStream_t stream);
 int flow2_waves_per_cu(int C);

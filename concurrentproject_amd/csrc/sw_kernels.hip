@@ -177,17 +177,11 @@ __device__ __forceinline__ int code_of(unsigned raw, int k0, int lane, int C, in
 
 // Publish the right-edge outflow collected in lanes [64-C, 64) of a chunk that
 // started at step k0: rows k0 - (64W-1) .. k0 + C - 1 - (64W-1).
-template <int W, int C>
-__device__ __forceinline__ void publish_granules(const unsigned epoch, const __amdgpu_buffer_rsrc_t out_rsrc, int k0,
-                                                 int lane, int m, int IOH, int IOE) {
+template <int W, int C, int AUX = AUX_SC1>
+__device__ __forceinline__ void publish_granules(const Edge& out, int k0, int lane, int m, int IOH, int IOE) {
     const int row_out = k0 + (lane - (64 - C)) - (64 * W - 1);
     const bool st = lane >= 64 - C && row_out >= 0 && row_out < m;
-    u32x4 g;
-    g.x = epoch;
-    g.y = (unsigned)IOH;
-    g.z = (unsigned)IOE;
-    g.w = granule_chk(epoch, IOH, IOE, row_out);
-    __builtin_amdgcn_raw_buffer_store_b128(g, out_rsrc, st ? (unsigned)row_out * 16u : OOR, 0, AUX_SC1);
+    edge_publish<AUX>(out, row_out, st, IOH, IOE);
 }
 
 // One full strip pass with granule inflow (strip > 0) and outflow (strip < strips-1).
@@ -203,28 +197,28 @@ __device__ void strip_pass(const KParams& kp, const PairDesc& pd, const int stri
 
     const bool has_in = strip > 0;
     const bool has_out = strip < pd.strips - 1;
-    const __amdgpu_buffer_rsrc_t in_rsrc = bnd_rsrc(kp, pd, strip - 1);
-    const __amdgpu_buffer_rsrc_t out_rsrc = bnd_rsrc(kp, pd, strip);
+    const Edge in_e = strip_edge(kp, pd, strip - 1);
+    const Edge out_e = strip_edge(kp, pd, strip);
     const __amdgpu_buffer_rsrc_t row_rsrc =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned char*>(kp.seq + pd.row_off), 0, m, RSRC_FLAGS);
 
     const int nchunks = (m + SW - 1 + C - 1) / C;
     bool failed = false;
     unsigned raw_nxt = fetch_raw(row_rsrc, 0, lane, C, m);
-    u32x4 g_nxt = has_in ? fetch_granules<C>(in_rsrc, 0, lane, m) : u32x4{0u, 0u, 0u, 0u};
+    u32x4 g_nxt = has_in ? fetch_granules<C>(in_e, 0, lane, m) : u32x4{0u, 0u, 0u, 0u};
     for (int c = 0; c < nchunks; ++c) {
         const int k0 = c * C;
         const unsigned raw = raw_nxt;
         u32x4 g = g_nxt;
         // next chunk's rows in flight while this chunk computes
         raw_nxt = fetch_raw(row_rsrc, k0 + C, lane, C, m);
-        if (has_in) await_granules<C>(kp, in_rsrc, g, k0, lane, m, strip, failed, kp.epoch);
-        if (has_in) g_nxt = fetch_granules<C>(in_rsrc, k0 + C, lane, m);
+        if (has_in) await_granules<C>(kp, in_e, g, k0, lane, m, strip, failed);
+        if (has_in) g_nxt = fetch_granules<C>(in_e, k0 + C, lane, m);
         const int code = code_of<DNA>(raw, k0, lane, C, m);
         const bool real = has_in && k0 + lane < m;
         S.feed(lane, C, real ? (int)g.y : -go, real ? (int)g.z : -ge, code);
         S.template run<C>(l63, go, ge, ma, mi);
-        if (has_out) publish_granules<W, C>(kp.epoch, out_rsrc, k0, lane, m, S.IOH, S.IOE);
+        if (has_out) publish_granules<W, C>(out_e, k0, lane, m, S.IOH, S.IOE);
     }
     S.commit_max(kp, pd, lane);
 }
@@ -305,9 +299,8 @@ __global__ void __launch_bounds__(256) sw_chain_kernel(KParams kp) {
         const bool lin = real && wave > 0;
         const bool lout = real && wave < 3 && strip + 1 < pd.strips;
         // granule buffers exist only between groups: boundary g joins group g and g+1
-        const __amdgpu_buffer_rsrc_t in_rsrc = group_rsrc(kp, pd, group - 1, ngroups);
-        const __amdgpu_buffer_rsrc_t out_rsrc = group_rsrc(kp, pd, group, ngroups);
-        const unsigned ep_in = group_epoch(kp, group - 1, ngroups), ep_out = group_epoch(kp, group, ngroups);
+        const Edge in_e = group_edge(kp, pd, group - 1, ngroups);
+        const Edge out_e = group_edge(kp, pd, group, ngroups);
         const __amdgpu_buffer_rsrc_t row_rsrc =
             __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned char*>(kp.seq + pd.row_off), 0, m, RSRC_FLAGS);
         const int nloc = (m + SW - 1 + C - 1) / C;
@@ -323,20 +316,23 @@ __global__ void __launch_bounds__(256) sw_chain_kernel(KParams kp) {
         // granule role so that its global loads/stores are unconditional (rows
         // outside the chunk's range are predicated by the OOR offset) and the
         // compiler can count vmcnt exactly instead of draining at every join.
+        // gin_c / gout_c: 0 (no granule edge) or the edge's cache policy (AUX_SC1, or
+        // AUX_SYS for a slab edge to / from another GPU)
         auto chunk_loop = [&](auto gin_c, auto gout_c) __attribute__((always_inline)) {
-            constexpr bool GIN = decltype(gin_c)::value, GOUT = decltype(gout_c)::value;
+            constexpr int GIN_AUX = decltype(gin_c)::value, GOUT_AUX = decltype(gout_c)::value;
+            constexpr bool GIN = GIN_AUX != 0, GOUT = GOUT_AUX != 0;
             unsigned r0 = fetch_raw(row_rsrc, c * C, lane, C, m), r1 = fetch_raw(row_rsrc, c * C + C, lane, C, m);
             u32x4 g0 = u32x4{0u, 0u, 0u, 0u}, g1 = g0;
             if constexpr (GIN) {
-                g0 = fetch_granules<C>(in_rsrc, c * C, lane, m);
-                g1 = fetch_granules<C>(in_rsrc, c * C + C, lane, m);
+                g0 = fetch_granules<C, GIN_AUX>(in_e, c * C, lane, m);
+                g1 = fetch_granules<C, GIN_AUX>(in_e, c * C + C, lane, m);
             }
             auto chunk = [&](const int cc, u32x4& gbuf, unsigned& rbuf) __attribute__((always_inline)) {
                 const int k0 = cc * C;
                 const bool active = cc >= 0 && cc < nloc;
                 // consume the buffers before refilling them, so each refill can
                 // land in the registers the loop carries (no back-edge copies)
-                if constexpr (GIN) await_granules<C>(kp, in_rsrc, gbuf, k0, lane, m, strip, failed, ep_in);
+                if constexpr (GIN) await_granules<C, GIN_AUX>(kp, in_e, gbuf, k0, lane, m, strip, failed);
                 const int code = code_of<DNA>(rbuf, k0, lane, C, m);
                 int hg_in = -go, eh_in = -ge;
                 const int row = k0 + lane;
@@ -349,11 +345,11 @@ __global__ void __launch_bounds__(256) sw_chain_kernel(KParams kp) {
                     }
                 }
                 rbuf = fetch_raw(row_rsrc, k0 + 2 * C, lane, C, m);
-                if constexpr (GIN) gbuf = fetch_granules<C>(in_rsrc, k0 + 2 * C, lane, m);
+                if constexpr (GIN) gbuf = fetch_granules<C, GIN_AUX>(in_e, k0 + 2 * C, lane, m);
                 S.feed(lane, C, hg_in, eh_in, code);
                 S.template run<C>(l63, go, ge, ma, mi);
                 if constexpr (GOUT) {
-                    publish_granules<W, C>(ep_out, out_rsrc, k0, lane, m, S.IOH, S.IOE);
+                    publish_granules<W, C, GOUT_AUX>(out_e, k0, lane, m, S.IOH, S.IOE);
                 } else if (active && lout) {
                     const int row_out = k0 + (lane - (64 - C)) - (SW - 1);
                     if (lane >= 64 - C && row_out >= 0 && row_out < m) ring[wave][row_out & (R - 1)] = make_int2(S.IOH, S.IOE);
@@ -367,12 +363,24 @@ __global__ void __launch_bounds__(256) sw_chain_kernel(KParams kp) {
             }
             if (T < nT) chunk(c, g0, r0);
         };
-        using T_ = std::true_type;
-        using F_ = std::false_type;
-        if (gin && gout) chunk_loop(T_{}, T_{});   // a one-strip group between two slab edges
-        else if (gin) chunk_loop(T_{}, F_{});
-        else if (gout) chunk_loop(F_{}, T_{});
-        else chunk_loop(F_{}, F_{});
+        using N_ = std::integral_constant<int, 0>;
+        using D_ = std::integral_constant<int, AUX_SC1>;
+        using P_ = std::integral_constant<int, AUX_SYS>;
+        const bool gin_peer = gin && strip == 0, gout_peer = gout && last && kp.slab_out != nullptr;
+        if (gin && gout) {   // a one-strip group between two group or slab edges
+            if (gin_peer && gout_peer) chunk_loop(P_{}, P_{});
+            else if (gin_peer) chunk_loop(P_{}, D_{});
+            else if (gout_peer) chunk_loop(D_{}, P_{});
+            else chunk_loop(D_{}, D_{});
+        } else if (gin) {
+            if (gin_peer) chunk_loop(P_{}, N_{});
+            else chunk_loop(D_{}, N_{});
+        } else if (gout) {
+            if (gout_peer) chunk_loop(N_{}, P_{});
+            else chunk_loop(N_{}, D_{});
+        } else {
+            chunk_loop(N_{}, N_{});
+        }
         if (real) S.commit_max(kp, pd, lane);
     }
 }
@@ -473,13 +481,12 @@ __global__ void __launch_bounds__(256) sw_flow_kernel(KParams kp) {
         Strip<W, true> S;
         S.setup(kp, pd, strip, lane);
         const int ngroups = (pd.strips + 3) / 4;
-        const int in_kind = wave > 0 ? FLOW_LDS : (strip > 0 || kp.slab_in != nullptr) ? FLOW_GRANULE : FLOW_NONE;
-        const int out_kind = strip + 1 >= pd.strips ? (kp.slab_out != nullptr ? FLOW_GRANULE : FLOW_NONE)
+        const int in_kind = wave > 0 ? FLOW_LDS : strip > 0 ? FLOW_GRANULE : kp.slab_in != nullptr ? FLOW_PEER : FLOW_NONE;
+        const int out_kind = strip + 1 >= pd.strips ? (kp.slab_out != nullptr ? FLOW_PEER : FLOW_NONE)
                              : wave < 3           ? FLOW_LDS
                                                   : FLOW_GRANULE;
-        const __amdgpu_buffer_rsrc_t in_rsrc = group_rsrc(kp, pd, group - 1, ngroups);
-        const __amdgpu_buffer_rsrc_t out_rsrc = group_rsrc(kp, pd, group, ngroups);
-        const unsigned ep_in = group_epoch(kp, group - 1, ngroups), ep_out = group_epoch(kp, group, ngroups);
+        const Edge in_e = group_edge(kp, pd, group - 1, ngroups);
+        const Edge out_e = group_edge(kp, pd, group, ngroups);
         const int nloc = (m + SW - 1 + C - 1) / C;
         bool failed = false;
         const long long t_start = (long long)__builtin_amdgcn_s_memrealtime();
@@ -492,10 +499,11 @@ __global__ void __launch_bounds__(256) sw_flow_kernel(KParams kp) {
         int* const cons_out = lane == 0 ? &cons[wave] : &sink[wave][lane];
         auto flow_loop = [&](auto in_c, auto out_c) __attribute__((always_inline)) {
             constexpr int IN = decltype(in_c)::value, OUT = decltype(out_c)::value;
+            constexpr int AIN = flow_aux(IN), AOUT = flow_aux(OUT);
             u32x4 g0 = u32x4{0u, 0u, 0u, 0u}, g1 = g0;
-            if constexpr (IN == FLOW_GRANULE) {
-                g0 = fetch_granules<C>(in_rsrc, 0, lane, m);
-                if constexpr (SW_GPREF == 2) g1 = fetch_granules<C>(in_rsrc, C, lane, m);
+            if constexpr (flow_granule(IN)) {
+                g0 = fetch_granules<C, AIN>(in_e, 0, lane, m);
+                if constexpr (SW_GPREF == 2) g1 = fetch_granules<C, AIN>(in_e, C, lane, m);
             }
             unsigned code_nxt = rc[lane];
             int cons_seen = 0;   // OUT == FLOW_LDS: last value read of the consumer's word
@@ -514,15 +522,15 @@ __global__ void __launch_bounds__(256) sw_flow_kernel(KParams kp) {
                 }
 #endif
                 int hg_in = -go, eh_in = -ge;
-                if constexpr (IN == FLOW_GRANULE) {
-                    await_granules<C>(kp, in_rsrc, gbuf, k0, lane, m, strip, failed, ep_in);
+                if constexpr (flow_granule(IN)) {
+                    await_granules<C, AIN>(kp, in_e, gbuf, k0, lane, m, strip, failed);
                     const bool live = row < m;
                     hg_in = live ? (int)gbuf.y : -go;
                     eh_in = live ? (int)gbuf.z : -ge;
 #ifdef SW_TIMELINE
                     if (c == 0) t_first = (long long)__builtin_amdgcn_s_memrealtime();
 #endif
-                    gbuf = fetch_granules<C>(in_rsrc, k0 + SW_GPREF * C, lane, m);
+                    gbuf = fetch_granules<C, AIN>(in_e, k0 + SW_GPREF * C, lane, m);
                 } else if constexpr (IN == FLOW_LDS) {
                     const int need = min(k0 + C, m);
                     // the progress word and the rows behind it in one round trip;
@@ -558,8 +566,8 @@ __global__ void __launch_bounds__(256) sw_flow_kernel(KParams kp) {
                 const unsigned long long ts1 = SW_STAMP();
                 S.template run<C>(l63, go, ge, ma, mi);
                 const unsigned long long ts2 = SW_STAMP();
-                if constexpr (OUT == FLOW_GRANULE) {
-                    publish_granules<W, C>(ep_out, out_rsrc, k0, lane, m, S.IOH, S.IOE);
+                if constexpr (flow_granule(OUT)) {
+                    publish_granules<W, C, AOUT>(out_e, k0, lane, m, S.IOH, S.IOE);
                 } else if constexpr (OUT == FLOW_LDS) {
                     const int hi = k0 + C - SW;   // last row this chunk completes
                     if (hi >= 0) {
@@ -598,22 +606,7 @@ __global__ void __launch_bounds__(256) sw_flow_kernel(KParams kp) {
             }
             if (c < nloc) chunk(c, g0);
         };
-        using I0 = std::integral_constant<int, FLOW_NONE>;
-        using I1 = std::integral_constant<int, FLOW_GRANULE>;
-        using I2 = std::integral_constant<int, FLOW_LDS>;
-        if (in_kind == FLOW_LDS) {
-            if (out_kind == FLOW_LDS) flow_loop(I2{}, I2{});
-            else if (out_kind == FLOW_GRANULE) flow_loop(I2{}, I1{});
-            else flow_loop(I2{}, I0{});
-        } else if (in_kind == FLOW_GRANULE) {
-            if (out_kind == FLOW_LDS) flow_loop(I1{}, I2{});
-            else if (out_kind == FLOW_GRANULE) flow_loop(I1{}, I1{});   // one-strip group between slab edges
-            else flow_loop(I1{}, I0{});
-        } else {
-            if (out_kind == FLOW_LDS) flow_loop(I0{}, I2{});
-            else if (out_kind == FLOW_GRANULE) flow_loop(I0{}, I1{});   // a one-strip first slab
-            else flow_loop(I0{}, I0{});
-        }
+        dispatch_kinds(in_kind, out_kind, flow_loop);
         if (kp.trace != nullptr && lane == 0) {
             unsigned long long* t = kp.trace + 16ull * (unsigned)strip;
             t[0] = (unsigned long long)t_start;
@@ -823,8 +816,8 @@ __device__ void strip_pass_duo(const KParams& kp, const DuoDesc& d, const int st
     const bool has_out = strip < d.strips - 1;
     Granule* in_base = kp.bnd + d.bnd_off + (uint64_t)(has_in ? strip - 1 : 0) * (uint64_t)m;
     Granule* out_base = kp.bnd + d.bnd_off + (uint64_t)strip * (uint64_t)m;
-    const __amdgpu_buffer_rsrc_t in_rsrc = __builtin_amdgcn_make_buffer_rsrc(in_base, 0, m * 16, RSRC_FLAGS);
-    const __amdgpu_buffer_rsrc_t out_rsrc = __builtin_amdgcn_make_buffer_rsrc(out_base, 0, m * 16, RSRC_FLAGS);
+    const Edge in_e = linear_edge(in_base, m, kp.epoch);
+    const Edge out_e = linear_edge(out_base, m, kp.epoch);
     const __amdgpu_buffer_rsrc_t r0 =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned char*>(kp.seq + d.row_off[0]), 0, d.m[0], RSRC_FLAGS);
     const __amdgpu_buffer_rsrc_t r1 =
@@ -832,15 +825,15 @@ __device__ void strip_pass_duo(const KParams& kp, const DuoDesc& d, const int st
     const int nchunks = (m + SW - 1 + C - 1) / C;
     bool failed = false;
     unsigned raw0_nxt = fetch_raw(r0, 0, lane, C, d.m[0]), raw1_nxt = fetch_raw(r1, 0, lane, C, d.m[1]);
-    u32x4 g_nxt = has_in ? fetch_granules<C>(in_rsrc, 0, lane, m) : u32x4{0u, 0u, 0u, 0u};
+    u32x4 g_nxt = has_in ? fetch_granules<C>(in_e, 0, lane, m) : u32x4{0u, 0u, 0u, 0u};
     for (int c = 0; c < nchunks; ++c) {
         const int k0 = c * C;
         const unsigned raw0 = raw0_nxt, raw1 = raw1_nxt;
         u32x4 g = g_nxt;
         raw0_nxt = fetch_raw(r0, k0 + C, lane, C, d.m[0]);
         raw1_nxt = fetch_raw(r1, k0 + C, lane, C, d.m[1]);
-        if (has_in) await_granules<C>(kp, in_rsrc, g, k0, lane, m, strip, failed, kp.epoch);
-        if (has_in) g_nxt = fetch_granules<C>(in_rsrc, k0 + C, lane, m);
+        if (has_in) await_granules<C>(kp, in_e, g, k0, lane, m, strip, failed);
+        if (has_in) g_nxt = fetch_granules<C>(in_e, k0 + C, lane, m);
         const unsigned code = codes_duo(raw0, raw1, k0, lane, C, d);
         if (lane < C) {
             const bool real = has_in && k0 + lane < m;
@@ -849,7 +842,7 @@ __device__ void strip_pass_duo(const KParams& kp, const DuoDesc& d, const int st
             S.IOR = code;
         }
         S.template run<C>(go2, ge2, ma2, gom2);
-        if (has_out) publish_granules<W, C>(kp.epoch, out_rsrc, k0, lane, m, (int)S.IOA, (int)S.IOE);
+        if (has_out) publish_granules<W, C>(out_e, k0, lane, m, (int)S.IOA, (int)S.IOE);
     }
     S.commit_max(kp, d, lane);
 }
@@ -887,12 +880,9 @@ hipError_t launch_t(const LaunchCfg& cfg, const KParams& kp, hipStream_t s) {
             if constexpr (DNA) {
                 const int dyn = flow_stage_rows(cfg.max_m, W, C);
                 if (dyn > flow_stage_max(W, C)) return hipErrorInvalidValue;
-                static int dyn_set = 0;   // raise the dynamic-LDS limit once per variant
-                if (dyn > 64 * 1024 && dyn_set == 0) {
-                    const hipError_t e = hipFuncSetAttribute((const void*)sw_flow_kernel<W, C>,
-                                                             hipFuncAttributeMaxDynamicSharedMemorySize, flow_stage_max(W, C));
+                if (dyn > 64 * 1024) {   // raise the dynamic-LDS limit (once per variant and device)
+                    const hipError_t e = raise_dyn_lds((const void*)sw_flow_kernel<W, C>, flow_stage_max(W, C));
                     if (e != hipSuccess) return e;
-                    dyn_set = 1;
                 }
                 hipLaunchKernelGGL((sw_flow_kernel<W, C>), dim3(cfg.blocks), dim3(256), (size_t)dyn, s, kp);
                 break;

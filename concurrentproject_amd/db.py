@@ -89,8 +89,20 @@ class Database:
         _check(lib().sw_db_record(self._h, int(i), ctypes.byref(seq), ctypes.byref(n), ctypes.byref(hdr)))
         return hdr.value.decode("latin-1"), ctypes.string_at(seq, n.value) if n.value else b""
 
+    def length(self, i: int) -> int:
+        """Residues of record i (no copy: sw_db_record with seq = NULL)."""
+        n = ctypes.c_int()
+        _check(lib().sw_db_record(self._h, int(i), None, ctypes.byref(n), None))
+        return n.value
+
+    def header(self, i: int) -> str:
+        """Header of record i (no residue copy)."""
+        hdr = ctypes.c_char_p()
+        _check(lib().sw_db_record(self._h, int(i), None, None, ctypes.byref(hdr)))
+        return hdr.value.decode("latin-1")
+
     def lengths(self) -> np.ndarray:
-        return np.array([len(self.record(i)[1]) for i in range(len(self))], dtype=np.int64)
+        return np.array([self.length(i) for i in range(len(self))], dtype=np.int64)
 
     # ---- search ---------------------------------------------------------------
     def search(self, query) -> np.ndarray:
@@ -110,4 +122,4 @@ class Database:
         """The k best records: [(score, index, header)], score descending, index ascending on ties."""
         sc = self.search(query)
         idx = np.lexsort((np.arange(len(sc)), -sc.astype(np.int64)))[:k]
-        return [(int(sc[i]), int(i), self.record(int(i))[0]) for i in idx]
+        return [(int(sc[i]), int(i), self.header(int(i))) for i in idx]

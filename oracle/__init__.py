@@ -41,6 +41,8 @@ class Params:
 
 
 DEFAULT = Params()
+# constants of the param-substituted reference builds (oracle/Makefile refvar)
+REFVAR_PARAMS = (Params(2, -3, 5, 2), Params(1, -1, 3, 1))
 _lib = None
 
 
@@ -49,6 +51,10 @@ def build() -> None:
     subprocess.run(["make", "-s", "-C", HERE, "all"], check=True)
     if os.path.isdir("/root/reference"):
         subprocess.run(["make", "-s", "-C", HERE, "ref"], check=True)
+        # param-substituted reference builds (G_INIT != G_EXT), for the long-pair pins
+        for prm in REFVAR_PARAMS:
+            subprocess.run(["make", "-s", "-C", HERE, "refvar", "MA=%d" % prm.match, "MI=%d" % prm.mismatch,
+                            "GI=%d" % prm.gap_init, "GE=%d" % prm.gap_ext], check=True)
         # the reference harness linked against the MI355X library (needs it built)
         if os.path.exists(os.path.join(HERE, "..", "concurrentproject_amd", "libswmi355.so")):
             subprocess.run(["make", "-s", "-C", HERE, "harness"], check=True)

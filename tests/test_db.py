@@ -111,6 +111,41 @@ def test_database_errors(sw, tmp_path):
         sw.Database.open(tmp_path / "cut.swdb")
     with pytest.raises(sw.SwError, match="no such record"):
         db.record(2)
+    assert [db.length(i) for i in range(2)] == [4, 2] and db.header(1) == "b"
+
+
+def test_database_crafted_files(sw, tmp_path):
+    """Binary files whose sizes would wrap a sum: rejected, never read past the end."""
+    import struct
+    db = sw.Database.from_fasta(b">a\nACGT\n>b\nGG\n")
+    db.save(tmp_path / "ok.swdb")
+    blob = (tmp_path / "ok.swdb").read_bytes()
+    magic = blob[:8]
+    hdr_len_2 = len(b"a") + len(b"b")
+    table = blob[32:32 + 2 * 16]
+    body = blob[32 + 2 * 16:]
+
+    def craft(name, count, nres, hbytes, recs, tail):
+        raw = magic + struct.pack("<QQQ", count, nres, hbytes)
+        for off, ln, hl in recs:
+            raw += struct.pack("<qii", off, ln, hl)
+        (tmp_path / name).write_bytes(raw + tail)
+        return tmp_path / name
+
+    # one header length near 2^31 and nres chosen so that p + hbytes + nres wraps to the file size
+    big = 0x7FFFFFF0
+    p = 32 + 16
+    size = p + 10
+    nres = (size - p - big) % (1 << 64)
+    f = craft("wrap.swdb", 1, nres, big, [(0, 0, big)], b"x" * 10)
+    with pytest.raises(sw.SwError, match="truncated"):
+        sw.Database.open(f)
+    # a record whose residues run past nres
+    f = craft("past.swdb", 2, 6, hdr_len_2, [(0, 4, 1), (4, 3, 1)], body)
+    with pytest.raises(sw.SwError, match="truncated"):
+        sw.Database.open(f)
+    # the well-formed file still opens
+    assert len(sw.Database.open(tmp_path / "ok.swdb")) == 2 and table
 
 
 # ---- GPU: search parity ---------------------------------------------------------------

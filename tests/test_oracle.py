@@ -103,3 +103,38 @@ def test_restatement_vs_reference_build(oracle_mod):
             a = np.frombuffer(b"ACGT", np.uint8)[rng.integers(0, 4, n)]
             b = np.frombuffer(b"ACGT", np.uint8)[rng.integers(0, 4, m)]
             assert oracle_mod.score_linear(a, b, prm) == oracle_mod.ref_score(a, b, prm)
+
+
+def test_restatement_vs_reference_c3_size(oracle_mod, golden):
+    """Eight C3-size pairs (N = 8192, seeds 8192..8199): the restatement, the
+    reference's own LazySmith (lazySmith.cpp:15-69 compiled in place) and the
+    committed C3/C4 golden agree (the goldens were generated by the restatement,
+    swo_linear; this pins them to the reference at full config size)."""
+    if oracle_mod.ref_lib() is None:
+        pytest.skip("oracle/_ref not built (no /root/reference here)")
+    gold = golden("configs.json")["C3"]["scores"][:8]
+    for k in range(8):
+        a, b = oracle_mod.gen_pair(8192 + k, 8192)
+        r = oracle_mod.ref_score(a, b, which="lazy")
+        assert oracle_mod.score_linear(a, b) == r == gold[k], k
+
+
+def test_restatement_vs_reference_long_affine(oracle_mod):
+    """G_INIT != G_EXT on long pairs (3000-4000, similar sequences with indels, so
+    long gaps run through E and F): restatement == param-substituted builds of the
+    reference's main.cpp / lazySmith.cpp (oracle/Makefile refvar)."""
+    rng = np.random.default_rng(44)
+    for prm in oracle_mod.REFVAR_PARAMS:
+        if oracle_mod.ref_lib(prm) is None:
+            pytest.skip("refvar builds absent (make -C oracle refvar)")
+        for n, m in ((3000, 3300), (4000, 3700)):
+            a = np.frombuffer(b"ACGT", np.uint8)[rng.integers(0, 4, n)]
+            b = np.resize(a, m).copy()
+            mut = rng.random(m) < 0.08
+            b[mut] = np.frombuffer(b"ACGT", np.uint8)[rng.integers(0, 4, int(mut.sum()))]
+            for cut in sorted(rng.integers(10, m - 40, 6)):   # indels of 1..30 bases
+                ln = int(rng.integers(1, 30))
+                b = np.concatenate([b[:cut], b[cut + ln:], b[:ln]])[:m] if rng.random() < 0.5 else \
+                    np.concatenate([b[:cut], a[:ln], b[cut:]])[:m]
+            exp = oracle_mod.ref_score(a, b, prm, which="lazy")
+            assert oracle_mod.score_linear(a, b, prm) == exp == oracle_mod.ref_score(a, b, prm), (prm, n, m)

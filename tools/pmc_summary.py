@@ -2,21 +2,27 @@
 """Turn the rocprofv3 passes written by tools/prof_round.sh into the committed
 profile summaries.
 
-    python tools/pmc_summary.py gpurun_out/prof r01
+    python tools/pmc_summary.py gpurun_out/prof r02
 
 For each workload (c2 -> pair, c3 -> batch, c5 -> slab on one GPU):
-  * copies the kernel-trace stats and the FETCH_SIZE / WRITE_SIZE counter CSVs
-    and the bench line to profiles/<round>_<cfg>_*;
-  * writes profiles/pmc_<workload>.json, which bench.py reads for
-    roofline.traffic: HBM bytes per launch of the dominant engine kernel.
-    The counters were collected in separate --pmc passes, with no traces
-    combined.  Corrections follow MI355X_MICROARCH.md, HBM section:
-      - FETCH_SIZE counts half the bytes of 16-B/lane reads (the granule
-        reads), so it is doubled;
-      - WRITE_SIZE is exact for the 16-B/lane granule stores;
-      - the 1-B/lane row reads are uncalibrated (< 1% of the total).
+  * copies the kernel-trace stats, the counter CSVs and the bench line to
+    profiles/<round>_<cfg>_*;
+  * writes profiles/pmc_<workload>.json, which bench.py reads for its roofline,
+    stamped with the sha256 of the libswmi355.so that was profiled (bench.py
+    ignores a profile of another build).  Per launch of the dominant engine
+    kernel, averaged over the profiled dispatches:
+      - valu_insts_per_launch = SQ_INSTS_VALU (wave64 VALU instructions; the
+        roofline counts 64 lane-ops each);
+      - clock_ghz = GRBM_GUI_ACTIVE / 8 XCDs / kernel time (MI355X_MICROARCH.md,
+        DVFS give-back);
+      - hbm_bytes_per_launch = 2 x FETCH_SIZE + WRITE_SIZE (KB x 1024): gfx950
+        FETCH_SIZE counts half the bytes of 16-B/lane reads (the granule
+        reads), WRITE_SIZE is exact for the 16-B/lane granule stores; the
+        1-B/lane row reads are uncalibrated (< 1 % of the total).
+    Every counter group came from its own --pmc pass with nothing traced.
 """
 import csv
+import hashlib
 import json
 import os
 import shutil
@@ -26,6 +32,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ALGO_BYTES_PER_CELL = 12
 CELLS = {"c2": 65536 * 65536, "c3": 1024 * 8192 * 8192, "c5": (1 << 20) * (1 << 20)}
 WORKLOAD = {"c2": "pair", "c3": "batch", "c5": "slab"}
+LIB = os.path.join(ROOT, "concurrentproject_amd", "libswmi355.so")
 
 
 def _rows(path):
@@ -38,11 +45,20 @@ def _engine_kernel(rows, key="Kernel_Name"):
     return max(set(names), key=names.count)
 
 
-def per_launch(path):
+def per_launch(path, counter=None):
+    """(kernel, mean counter value per dispatch, dispatches) of the engine kernel."""
     rows = _rows(path)
     k = _engine_kernel(rows)
-    vals = [float(r["Counter_Value"]) for r in rows if r["Kernel_Name"] == k]
+    vals = [float(r["Counter_Value"]) for r in rows
+            if r["Kernel_Name"] == k and (counter is None or r["Counter_Name"] == counter)]
     return k, sum(vals) / len(vals), len(vals)
+
+
+def sha256(path):
+    h = hashlib.sha256()
+    with open(path, "rb") as f:
+        h.update(f.read())
+    return h.hexdigest()
 
 
 def main():
@@ -50,39 +66,53 @@ def main():
     prof = os.path.join(ROOT, "profiles")
     for cfg in ("c2", "c3", "c5"):
         stats = os.path.join(src, "kt_" + cfg, cfg + "_kernel_stats.csv")
-        fetch = os.path.join(src, "fetch_" + cfg, cfg + "_counter_collection.csv")
-        write = os.path.join(src, "write_" + cfg, cfg + "_counter_collection.csv")
-        if not all(os.path.exists(p) for p in (stats, fetch, write)):
+        if not os.path.exists(stats):
             print("skip", cfg)
             continue
         shutil.copy(stats, os.path.join(prof, "%s_%s_kernel_stats.csv" % (rnd, cfg)))
-        shutil.copy(fetch, os.path.join(prof, "%s_%s_pmc_fetch.csv" % (rnd, cfg)))
-        shutil.copy(write, os.path.join(prof, "%s_%s_pmc_write.csv" % (rnd, cfg)))
         bench = os.path.join(src, "bench_%s.json" % cfg)
         if os.path.exists(bench):
             shutil.copy(bench, os.path.join(prof, "%s_bench_%s.json" % (rnd, cfg)))
-        k, fkb, nf = per_launch(fetch)
-        k2, wkb, nw = per_launch(write)
-        assert k == k2, (k, k2)
+        k = _engine_kernel(_rows(stats), key="Name")
         st = [r for r in _rows(stats) if r["Name"] == k][0]
-        read_raw = fkb * 1024
-        out = {
-            "kernel": k,
-            "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes (MI355X_MICROARCH.md HBM "
-                      "section); KB per dispatch averaged over %d/%d dispatches; FETCH_SIZE doubled for the 16-B/lane "
-                      "granule reads (gfx950 reports half of a wide coalesced read); 1-B/lane row reads uncalibrated"
-                      % (nf, nw),
-            "kernel_avg_ns": float(st["AverageNs"]),
-            "kernel_calls": int(st["Calls"]),
-            "fetch_size_kb": fkb,
-            "write_size_kb": wkb,
-            "read_bytes_raw": read_raw,
-            "read_bytes_corrected": 2 * read_raw,
-            "write_bytes": wkb * 1024,
-            "hbm_bytes_per_launch": 2 * read_raw + wkb * 1024,
-            "algorithmic_bytes_per_launch": CELLS[cfg] * ALGO_BYTES_PER_CELL,
-        }
-        out["traffic_over_algorithmic"] = out["hbm_bytes_per_launch"] / out["algorithmic_bytes_per_launch"]
+        t_ns = float(st["AverageNs"])
+        out = {"kernel": k, "lib_sha256": sha256(LIB), "kernel_avg_ns": t_ns, "kernel_calls": int(st["Calls"]),
+               "algorithmic_bytes_per_launch": CELLS[cfg] * ALGO_BYTES_PER_CELL, "cells_per_launch": CELLS[cfg]}
+        passes = []
+        fetch = os.path.join(src, "fetch_" + cfg, cfg + "_counter_collection.csv")
+        write = os.path.join(src, "write_" + cfg, cfg + "_counter_collection.csv")
+        if os.path.exists(fetch) and os.path.exists(write):
+            shutil.copy(fetch, os.path.join(prof, "%s_%s_pmc_fetch.csv" % (rnd, cfg)))
+            shutil.copy(write, os.path.join(prof, "%s_%s_pmc_write.csv" % (rnd, cfg)))
+            kf, fkb, nf = per_launch(fetch)
+            kw, wkb, nw = per_launch(write)
+            assert kf == kw == k, (kf, kw, k)
+            out.update(fetch_size_kb=fkb, write_size_kb=wkb, read_bytes_corrected=2 * fkb * 1024,
+                       write_bytes=wkb * 1024, hbm_bytes_per_launch=2 * fkb * 1024 + wkb * 1024)
+            out["traffic_over_algorithmic"] = out["hbm_bytes_per_launch"] / out["algorithmic_bytes_per_launch"]
+            passes.append("FETCH_SIZE (%d dispatches), WRITE_SIZE (%d)" % (nf, nw))
+        sq = os.path.join(src, "sq_" + cfg, cfg + "_counter_collection.csv")
+        if os.path.exists(sq):
+            shutil.copy(sq, os.path.join(prof, "%s_%s_pmc_sq.csv" % (rnd, cfg)))
+            names = sorted({r["Counter_Name"] for r in _rows(sq)})
+            for c in names:
+                kk, v, n = per_launch(sq, c)
+                assert kk == k, (kk, k)
+                out[c] = v
+            out["valu_insts_per_launch"] = out.get("SQ_INSTS_VALU")
+            out["valu_lane_ops_per_launch"] = out["valu_insts_per_launch"] * 64
+            out["valu_frac_at_2p4ghz"] = out["valu_lane_ops_per_launch"] / (t_ns * 1e-9) / (256 * 4 * 32 * 2.4e9)
+            out["valu_insts_per_cell"] = out["valu_insts_per_launch"] / CELLS[cfg]
+            passes.append(" ".join(names))
+        grbm = os.path.join(src, "grbm_" + cfg, cfg + "_counter_collection.csv")
+        if os.path.exists(grbm):
+            shutil.copy(grbm, os.path.join(prof, "%s_%s_pmc_grbm.csv" % (rnd, cfg)))
+            kk, g, n = per_launch(grbm, "GRBM_GUI_ACTIVE")
+            out["GRBM_GUI_ACTIVE"] = g
+            out["clock_ghz"] = g / 8 / t_ns
+            passes.append("GRBM_GUI_ACTIVE")
+        out["method"] = ("rocprofv3 --pmc, one pass per group, nothing else traced: " + "; ".join(passes) +
+                         "; kernel time from the --kernel-trace --stats run of the same command")
         with open(os.path.join(prof, "pmc_%s.json" % WORKLOAD[cfg]), "w") as f:
             json.dump(out, f, indent=1)
         print(cfg, json.dumps(out))
