@@ -67,6 +67,7 @@ def parse():
     ap.add_argument("--C", type=int, default=0)
     ap.add_argument("--mode", type=int, default=-1, help="engine option 'mode' (-1 = automatic plan)")
     ap.add_argument("--params", default="1,-1,1,1", help="MATCH,MISMATCH,G_INIT,G_EXT")
+    ap.add_argument("--opt", action="append", default=[], help="engine option key=value (sw_set_option)")
     return ap.parse_args()
 
 
@@ -284,6 +285,9 @@ def main():
         sw.set_option("C", args.C)
     if args.mode >= 0:
         sw.set_option("mode", args.mode)
+    for kv in args.opt:
+        k, v = kv.split("=")
+        sw.set_option(k, int(v))
     gold = load_golden()
     defaults = params == (1, -1, 1, 1)
 

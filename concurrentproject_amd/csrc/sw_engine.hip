@@ -57,7 +57,8 @@ std::mutex g_param_mu;
 Params g_params;
 
 std::atomic<long long> g_opt_W{0}, g_opt_C{0}, g_opt_bytes{0}, g_opt_timeout{30}, g_opt_blocks{0}, g_opt_orient{0},
-    g_opt_mode{-1}, g_opt_trace{0}, g_opt_duo_f16{1}, g_opt_f2stream{0}, g_opt_ring{-1}, g_opt_ring_rows{4096};
+    g_opt_mode{-1}, g_opt_trace{0}, g_opt_duo_f16{1}, g_opt_f2stream{0}, g_opt_ring{-1}, g_opt_ring_rows{4096}, g_opt_f2_wgs{0},
+    g_opt_linear{-1};
 
 // Longest sequence the engine takes: granule buffers of m rows keep m * 16 in the
 // 32-bit record count of a buffer resource (sw_device.h linear_edge).
@@ -506,9 +507,22 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
     // error fields once (afterwards only check_ctrl resets them, after reporting)
     if (c->ctrl.p != ctrl_before) HIPCHK(hipMemsetAsync(c->ctrl.p, 0, sizeof(Ctrl), s));
     // ring mode: every block resident (one workgroup per CU for flow2), rings sized by the grid
+    // flow2 workgroups per CU: the staged kernel (C2) keeps one (a lone wave per
+    // SIMD: its step latency is the critical path); the streamed kernel of a pair
+    // with many strip groups per CU (C5) is throughput-bound, and more waves per
+    // SIMD hide each other's issue latency (sw_flow2.hip launch_c sizes the LDS pad)
+    const bool f2s = job.mode == MODE_FLOW2 && (job.f2_stream || job.ring || edge != nullptr);
+    // Ring mode keeps one per CU: at 2 or 3 per CU its static deal timed out on C5
+    // (4162 groups; fine on 794), consistent with not every block being resident,
+    // which the deal needs -- and the gain measured with linear edges was 9 %.
+    int f2_wgs = 1;
+    if (f2s && !job.ring) {
+        const long long o = g_opt_f2_wgs.load();
+        f2_wgs = o > 0 ? (int)o : (job.item_base[np] >= 8 * c->cus ? F2_WGS_AUTO : 1);
+    }
     int ring_blocks = 0, wrap_rows = 0;
     if (job.ring) {
-        ring_blocks = std::min(job.item_base[np], c->cus);
+        ring_blocks = std::min(job.item_base[np], c->cus * f2_wgs);
         if (g_opt_blocks.load() > 0) ring_blocks = (int)std::min<long long>(g_opt_blocks.load(), job.item_base[np]);
         wrap_rows = 1;
         while (wrap_rows < job.pairs[0].m) wrap_rows *= 2;
@@ -538,7 +552,11 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
     for (const PairDesc& d : job.pairs) max_m = std::max(max_m, d.m);
     LaunchCfg cfg{job.W, job.C, job.dna, 0, job.mode, max_m};
     cfg.duo_f16 = job.mode == MODE_DUO && job.duo_f16;
-    cfg.f2_stream = job.mode == MODE_FLOW2 && job.f2_stream;
+    // flow2 ring and slab kernels always stream the row codes (sw_flow2.hip launch_v)
+    cfg.f2_stream = f2s;
+    cfg.f2_wgs = f2_wgs;
+    // G_INIT == G_EXT: the exact linear-gap step (sw_flow2.hip LIN), unless disabled
+    cfg.f2_lin = job.mode == MODE_FLOW2 && job.C == 32 && prm.gap_init == prm.gap_ext && g_opt_linear.load() != 0;
     const int wpc = waves_per_cu(c, cfg);
     const int items = job.item_base[np];
     long long blocks = g_opt_blocks.load();
@@ -551,13 +569,14 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
         blocks = std::min<long long>(want, cap);
         // flow2 holds one workgroup per CU (its LDS size forces it); a grid larger than
         // the CU count would only park extra workgroups until a CU frees up
-        if (job.mode == MODE_FLOW2) blocks = std::min<long long>(blocks, c->cus);
+        if (job.mode == MODE_FLOW2) blocks = std::min<long long>(blocks, (long long)c->cus * f2_wgs);
     }
     if (job.ring) {
         // the static item deal needs every block resident at once; flow2 pads its LDS to
         // more than half a CU's, so one workgroup per CU
-        if (ring_blocks > c->cus) {
-            set_err("flow2 ring mode needs all %d workgroups co-resident (one per CU, %d CUs)", ring_blocks, c->cus);
+        if (ring_blocks > c->cus * f2_wgs) {
+            set_err("flow2 ring mode needs all %d workgroups co-resident (%d per CU, %d CUs)", ring_blocks, f2_wgs,
+                    c->cus);
             return -1;
         }
         blocks = ring_blocks;
@@ -598,7 +617,7 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
         kp.wrap_rows = wrap_rows;
         kp.ring_cons = c->cons.p;
     }
-    if (edge) {
+    if (edge) {   // (flow2 then runs its slab kernel, which streams the row codes)
         kp.slab_in = edge->in;
         kp.slab_out = edge->out;
         kp.slab_epoch = edge->epoch;
@@ -617,7 +636,7 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
     t_stats.waves_per_cu = wpc;
     t_stats.items = items;
     t_stats.mode = job.mode;
-    t_stats.variant = (cfg.duo_f16 ? 1 : 0) | (cfg.f2_stream ? 2 : 0) | (job.ring ? 4 : 0);
+    t_stats.variant = (cfg.duo_f16 ? 1 : 0) | (cfg.f2_stream ? 2 : 0) | (job.ring ? 4 : 0) | (cfg.f2_lin ? 8 : 0);
     t_stats.boundary_bytes = (long long)(job.bnd_granules * sizeof(Granule));
     c->last = s;
     return 0;
@@ -1087,6 +1106,12 @@ int sw_set_option(const char* key, long long v) {
         g_opt_duo_f16 = v ? 1 : 0;
     } else if (k == "f2stream") {   // 1 = flow2 streams row codes even when they fit in LDS (tests)
         g_opt_f2stream = v ? 1 : 0;
+    } else if (k == "f2_wgs") {   // flow2 streamed kernel: workgroups per CU, 0 = auto, 1..4
+        if (v < 0 || v > 4) return -1;
+        g_opt_f2_wgs = v;
+    } else if (k == "linear") {   // G_INIT == G_EXT: -1 auto (the linear-gap step), 0 = the affine step
+        if (v < -1 || v > 0) return -1;
+        g_opt_linear = v;
     } else if (k == "ring") {   // flow2 one-pair group edges: -1 auto (rings above 1 GB of edges), 0 off, 1 on
         if (v < -1 || v > 1) return -1;
         g_opt_ring = v;
@@ -1114,6 +1139,8 @@ long long sw_get_option(const char* key) {
     if (k == "duo16") return g_opt_duo_f16;
     if (k == "f2stream") return g_opt_f2stream;
     if (k == "ring") return g_opt_ring;
+    if (k == "linear") return g_opt_linear;
+    if (k == "f2_wgs") return g_opt_f2_wgs;
     if (k == "ring_rows") return g_opt_ring_rows;
     return -1;
 }

@@ -96,11 +96,24 @@ __device__ __forceinline__ int sbyte(unsigned w) {
 // store the codes of chunk c+2 (two ds_write_b8).  The step loop is unchanged.
 constexpr int F2_CR = 256;
 
-// RING: ring-mode edges (KParams::ring_rows > 0; streamed codes only).  A separate
-// instantiation, so the linear-edge kernel carries none of its back-pressure code.
-template <int C, bool STREAM, bool RING>
+// RING: ring-mode edges (KParams::ring_rows > 0).  SLAB: a column slab with edges
+// to / from other GPUs (KParams::slab_in / slab_out, system-scope hand-off loops).
+// Separate instantiations, both with streamed codes, so the single-GPU linear-edge
+// kernel (C2) carries none of their code.
+//
+// LIN: G_INIT == G_EXT (the reference's default constants, main.cpp:20-23).  Then
+// E(i,j) = H(i,j-1) - G and F(i,j) = H(i-1,j) - G exactly: by induction
+// E(i,j-1) <= H(i,j-1) (H is a max over E), so max(E(i,j-1) - G, H(i,j-1) - G)
+// is the second term; the same for F.  The step keeps H only:
+//   t   = H(i-1,j-1) + s            (SDWA add, as above)
+//   hgL = wave_shr1(hgO)            lanes 1..63: H(i,j-1) - G; lane 0 the inflow row
+//   H   = max(max3(hgL, hgO, 0), t) hgO = H(i-1,j) - G of this lane's last step
+//   hgO = H - G
+// 6.75 VALU per step instead of 10.7; edges carry (H - G, H - G), which is also
+// the exact (H - G_INIT, E - G_EXT) an affine consumer expects at G_INIT == G_EXT.
+template <int C, bool STREAM, bool RING, bool SLAB, bool LIN>
 __global__ void __launch_bounds__(256) sw_flow2_kernel(KParams kp) {
-    static_assert(!RING || STREAM, "ring mode runs the streamed-codes kernel");
+    static_assert(!(RING || SLAB) || STREAM, "ring and slab kernels stream the row codes");
     static_assert(C % 4 == 0 && 64 % C == 0 && 2 * C + 64 <= F2_R, "chunk");
     // STREAM ring: during chunk c the reads span rows [k0 + C - 63, k0 + 2C) and the
     // writes rows [k0 + 2C, k0 + 3C): no slot is rewritten while still read
@@ -264,7 +277,7 @@ __global__ void __launch_bounds__(256) sw_flow2_kernel(KParams kp) {
                         }
                     }
                 }
-                edge_publish<AOUT>(out_e, row_out, st, IOH, IOE);
+                edge_publish<AOUT>(out_e, row_out, st, IOH, LIN ? IOH : IOE);
             };
             // ---- publish the last chunk's outflow: lane L >= 64 - C holds row k0 - 128 + L
             auto publish = [&](const int k0) __attribute__((always_inline)) {
@@ -284,7 +297,7 @@ __global__ void __launch_bounds__(256) sw_flow2_kernel(KParams kp) {
                         }
                     }
                     int2* const dst = lane >= 64 - C ? &out_ring[row_out & (R - 1)] : &sink[wave][lane];
-                    *dst = make_int2(IOH, IOE);
+                    *dst = make_int2(IOH, LIN ? IOH : IOE);
                     compiler_fence();
                     *prod_out = max(0, k0 - 64);   // after the ring writes (in-order DS)
                 } else if constexpr (flow_granule(OUT)) {
@@ -411,25 +424,40 @@ __global__ void __launch_bounds__(256) sw_flow2_kernel(KParams kp) {
                             compiler_fence();
                         }
                     }
-                    auto step = [&](auto b_c) __attribute__((always_inline)) {
+                    auto step_lin = [&](auto b_c) __attribute__((always_inline)) {
                         constexpr int b = decltype(b_c)::value;
                         const int t = L0 + sbyte<b>(P[j >> 2]);
-                        // rotate the I/O registers down one lane; lane 63 takes last step's
-                        // (hgL, ehL) = row k - 64 of the next strip's lane 0
                         const int ioh = __builtin_amdgcn_update_dpp(L0, IOH, DPP_WAVE_SHL1, 0xF, 0xF, false);
-                        const int ioe = __builtin_amdgcn_update_dpp(ehP, IOE, DPP_WAVE_SHL1, 0xF, 0xF, false);
-                        const int F = max3i(fh, hgO, 0);
-                        const int hgL = dpp_add_shr1_tied(IOH, H, neggo, F);     // H -> hgO -> F -> DPP
-                        const int ehL = dpp_add_shr1_tied(IOE, E, negge, hgO);   // E -> H -> hgO -> DPP
+                        const int hgL = __builtin_amdgcn_update_dpp(IOH, hgO, DPP_WAVE_SHR1, 0xF, 0xF, false);
                         IOH = ioh;
-                        IOE = ioe;
-                        E = max3i(ehL, hgL, 0);
-                        fh = F - ge;
-                        H = vmax3(t, E, F);
+                        H = max(vmax3(hgL, hgO, 0), t);
                         hgO = H - go;
                         M = max(M, t);
                         L0 = hgL;
-                        ehP = ehL;
+                    };
+                    auto step = [&](auto b_c) __attribute__((always_inline)) {
+                        constexpr int b = decltype(b_c)::value;
+                        if constexpr (LIN) {
+                            step_lin(b_c);
+                        } else {
+                            const int t = L0 + sbyte<b>(P[j >> 2]);
+                            // rotate the I/O registers down one lane; lane 63 takes last step's
+                            // (hgL, ehL) = row k - 64 of the next strip's lane 0
+                            const int ioh = __builtin_amdgcn_update_dpp(L0, IOH, DPP_WAVE_SHL1, 0xF, 0xF, false);
+                            const int ioe = __builtin_amdgcn_update_dpp(ehP, IOE, DPP_WAVE_SHL1, 0xF, 0xF, false);
+                            const int F = max3i(fh, hgO, 0);
+                            const int hgL = dpp_add_shr1_tied(IOH, H, neggo, F);     // H -> hgO -> F -> DPP
+                            const int ehL = dpp_add_shr1_tied(IOE, E, negge, hgO);   // E -> H -> hgO -> DPP
+                            IOH = ioh;
+                            IOE = ioe;
+                            E = max3i(ehL, hgL, 0);
+                            fh = F - ge;
+                            H = vmax3(t, E, F);
+                            hgO = H - go;
+                            M = max(M, t);
+                            L0 = hgL;
+                            ehP = ehL;
+                        }
                     };
                     step(std::integral_constant<int, 0>{});
                     step(std::integral_constant<int, 1>{});
@@ -439,7 +467,7 @@ __global__ void __launch_bounds__(256) sw_flow2_kernel(KParams kp) {
             }
             publish(nloc * C);
         };
-        dispatch_kinds(in_kind, out_kind, flow_loop);
+        dispatch_kinds<SLAB>(in_kind, out_kind, flow_loop);
         if (kp.trace != nullptr && lane == 0) {
             unsigned long long* t = kp.trace + 16ull * (unsigned)strip;
             t[0] = (unsigned long long)t_start;
@@ -459,27 +487,40 @@ __global__ void __launch_bounds__(256) sw_flow2_kernel(KParams kp) {
     }
 }
 
-template <int C, bool STREAM, bool RING = false>
+template <int C, bool STREAM, bool RING = false, bool SLAB = false, bool LIN = false>
 hipError_t launch_c(const LaunchCfg& cfg, const KParams& kp, hipStream_t s) {
     // at least half the CU's LDS: one workgroup per CU, so no strip ever shares a
     // SIMD with another (a co-resident waiting workgroup's polls steal issue slots
     // from a strip on the critical path); STREAM stages nothing, the rest is padding
-    const int pad = LDS_PER_CU / 2 + 1024 - flow2_static_lds(C);
+    // STREAM: cfg.f2_wgs workgroups per CU (LDS just above 1/(wgs+1) of the CU's)
+    const int wgs = STREAM ? std::max(1, std::min(cfg.f2_wgs, 4)) : 1;
+    const int pad = LDS_PER_CU / (wgs + 1) + 1024 - flow2_static_lds(C);
     const int dyn = STREAM ? pad : std::max(flow2_stage_bytes(cfg.max_m, C), pad);
     const int lim = flow2_stage_max(C) - (STREAM ? 4 * (F2_CR + C + 64) : 0);
     if (dyn > lim) return hipErrorInvalidValue;
     if (dyn > 64 * 1024) {   // raise the dynamic-LDS limit (once per variant and device)
-        const hipError_t e = raise_dyn_lds((const void*)sw_flow2_kernel<C, STREAM, RING>, lim);
+        const hipError_t e = raise_dyn_lds((const void*)sw_flow2_kernel<C, STREAM, RING, SLAB, LIN>, lim);
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL((sw_flow2_kernel<C, STREAM, RING>), dim3(cfg.blocks), dim3(256), (size_t)dyn, s, kp);
+    hipLaunchKernelGGL((sw_flow2_kernel<C, STREAM, RING, SLAB, LIN>), dim3(cfg.blocks), dim3(256), (size_t)dyn, s,
+                       kp);
     return hipGetLastError();
+}
+
+// the instantiation a launch needs: ring edges, slab edges, streamed or staged codes
+template <int C, bool LIN>
+hipError_t launch_v(const LaunchCfg& cfg, const KParams& kp, hipStream_t s) {
+    const bool ring = kp.ring_rows > 0, slab = kp.slab_in != nullptr || kp.slab_out != nullptr;
+    if (slab)
+        return ring ? launch_c<C, true, true, true, LIN>(cfg, kp, s) : launch_c<C, true, false, true, LIN>(cfg, kp, s);
+    if (ring) return launch_c<C, true, true, false, LIN>(cfg, kp, s);
+    return cfg.f2_stream ? launch_c<C, true, false, false, LIN>(cfg, kp, s) : launch_c<C, false, false, false, LIN>(cfg, kp, s);
 }
 
 template <int C>
 int waves_c() {
     int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)sw_flow2_kernel<C, false, false>, 256, 0) != hipSuccess)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)sw_flow2_kernel<C, false, false, false, false>, 256, 0) != hipSuccess)
         return 4;
     return nb * 4;
 }
@@ -490,15 +531,10 @@ bool flow2_variant_exists(int C) { return C == 16 || C == 32 || C == 64; }
 
 hipError_t launch_sw_flow2(const LaunchCfg& cfg, const KParams& kp, hipStream_t stream) {
     switch (cfg.C) {
-        case 16: return kp.ring_rows > 0 ? launch_c<16, true, true>(cfg, kp, stream)
-                        : cfg.f2_stream  ? launch_c<16, true>(cfg, kp, stream)
-                                         : launch_c<16, false>(cfg, kp, stream);
-        case 32: return kp.ring_rows > 0 ? launch_c<32, true, true>(cfg, kp, stream)
-                        : cfg.f2_stream  ? launch_c<32, true>(cfg, kp, stream)
-                                         : launch_c<32, false>(cfg, kp, stream);
-        case 64: return kp.ring_rows > 0 ? launch_c<64, true, true>(cfg, kp, stream)
-                        : cfg.f2_stream  ? launch_c<64, true>(cfg, kp, stream)
-                                         : launch_c<64, false>(cfg, kp, stream);
+        // the linear-gap step (G_INIT == G_EXT) is built for the default chunk only
+        case 16: return launch_v<16, false>(cfg, kp, stream);
+        case 32: return cfg.f2_lin ? launch_v<32, true>(cfg, kp, stream) : launch_v<32, false>(cfg, kp, stream);
+        case 64: return launch_v<64, false>(cfg, kp, stream);
         default: return hipErrorInvalidValue;
     }
 }

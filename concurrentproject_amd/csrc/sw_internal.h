@@ -122,7 +122,10 @@ struct LaunchCfg {
     int max_m;      // longest row sequence (MODE_FLOW stages it in LDS)
     bool duo_f16 = false;   // MODE_DUO: max3 through v_pk_maximum3_f16 (every value < 0x7C00)
     bool f2_stream = false; // MODE_FLOW2: row codes streamed through per-wave LDS rings (rows too long to stage)
+    int f2_wgs = 1;         // MODE_FLOW2 streamed: workgroups per CU (LDS pad sized to admit exactly this many)
+    bool f2_lin = false;    // MODE_FLOW2, C = 32: the linear-gap step (G_INIT == G_EXT, exact; sw_flow2.hip LIN)
 };
+constexpr int F2_WGS_AUTO = 2;   // flow2 streamed kernel, many groups per CU: workgroups per CU
 
 // MODE_FLOW stages a pair's row codes in LDS: one byte per row plus the
 // prefetch tail; pairs whose rows do not fit use MODE_CHAIN.

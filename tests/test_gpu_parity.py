@@ -105,6 +105,14 @@ def test_config_c2_single_pair_65536(engine, golden):
         engine.set_option("C", C)
         assert engine.SmithWatermanScoreCUDA(a, b) == c["score"], C
     engine.set_option("C", 0)
+    # the affine step on the default constants (the automatic plan takes the exact
+    # linear-gap step, G_INIT == G_EXT) agrees at full size
+    engine.set_option("linear", 0)
+    assert engine.SmithWatermanScoreCUDA(a, b) == c["score"]
+    assert not engine.last_stats()["variant"] & 8
+    engine.set_option("linear", -1)
+    assert engine.SmithWatermanScoreCUDA(a, b) == c["score"]
+    assert engine.last_stats()["variant"] & 8
     engine.set_option("mode", -1)
     engine.set_option("W", 4)
     assert engine.SmithWatermanScoreCUDA(a, b) == c["score"]
@@ -188,16 +196,22 @@ def test_flow2_ragged(engine, oracle_mod):
     engine.set_option("orient", 1)   # keep (n, m) as given: seq1 across the lanes
     try:
         for prm in (engine.Params(), engine.Params(2, -3, 5, 2), engine.Params(1, -1, 3, 1), engine.Params(1, 0, 0, 0),
-                    engine.Params(60, -120, 67, 9)):
+                    engine.Params(60, -120, 67, 9), engine.Params(2, -3, 4, 4)):
             op = oracle_mod.Params(prm.match, prm.mismatch, prm.gap_init, prm.gap_ext)
             exp = [oracle_mod.score_linear(a, b, op) for a, b in pairs]
             engine.set_option("mode", 5)
             for C in (16, 32, 64):
                 engine.set_option("C", C)
-                got = [engine.score(a, b, prm) for a, b in pairs]
-                assert got == exp, (C, prm)
-                assert engine.last_stats()["mode"] == 5
-                assert engine.score_batch(pairs, prm) == exp, (C, prm)
+                # G_INIT == G_EXT at C = 32: the linear-gap step (auto) and the affine step (linear = 0)
+                for lin in ((-1, 0) if prm.gap_init == prm.gap_ext and C == 32 else (-1,)):
+                    engine.set_option("linear", lin)
+                    got = [engine.score(a, b, prm) for a, b in pairs]
+                    assert got == exp, (C, prm, lin)
+                    st = engine.last_stats()
+                    assert st["mode"] == 5
+                    assert bool(st["variant"] & 8) == (lin == -1 and prm.gap_init == prm.gap_ext and C == 32), st
+                    assert engine.score_batch(pairs, prm) == exp, (C, prm, lin)
+                engine.set_option("linear", -1)
             engine.set_option("C", 0)
             engine.set_option("blocks", 1)
             assert engine.score_batch(pairs, prm) == exp, prm

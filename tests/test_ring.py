@@ -49,7 +49,7 @@ def test_ring_mode_matches_oracle(engine, oracle_mod, stream):
     engine.set_option("mode", 5)
     engine.set_option("ring", 1)
     engine.set_option("f2stream", stream)
-    for prm in (engine.Params(), engine.Params(2, -3, 5, 2)):
+    for prm in (engine.Params(), engine.Params(2, -3, 5, 2), engine.Params(3, -2, 4, 4)):
         op = oracle_mod.Params(prm.match, prm.mismatch, prm.gap_init, prm.gap_ext)
         exp = [oracle_mod.score_linear(a, b, op) for a, b in pairs]
         for blocks, rows in ((0, 4096), (1, 512), (2, 512), (3, 1024), (7, 512)):

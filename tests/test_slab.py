@@ -144,7 +144,8 @@ def test_slabs_threads_every_kernel(engine, oracle_mod, nslabs):
             got, bounds, stats = _run_threads(engine, a, b, nslabs, flags)
             assert max(got) == exp, (name, n, m, got, exp, bounds)
             assert all(s["mode"] == want_mode for s in stats), (name, [s["mode"] for s in stats])
-            assert all(bool(s["variant"] & 2) == (name == "flow2-stream") for s in stats), name
+            # flow2 slabs run the slab kernel, which streams the row codes
+            assert all(bool(s["variant"] & 2) == name.startswith("flow2") for s in stats), name
             # a slab reports max(0, max t) over its cells (t = diagonal + s): an H that
             # comes from a gap opened in an earlier slab is counted there, so a slab's
             # value is at most the oracle's max H over its columns, and the pair's
