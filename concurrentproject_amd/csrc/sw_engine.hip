@@ -556,7 +556,8 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
     cfg.f2_stream = f2s;
     cfg.f2_wgs = f2_wgs;
     // G_INIT == G_EXT: the exact linear-gap step (sw_flow2.hip LIN), unless disabled
-    cfg.f2_lin = job.mode == MODE_FLOW2 && job.C == 32 && prm.gap_init == prm.gap_ext && g_opt_linear.load() != 0;
+    cfg.f2_lin = ((job.mode == MODE_FLOW2 && job.C == 32) || (job.mode == MODE_DUO && cfg.duo_f16)) &&
+                 prm.gap_init == prm.gap_ext && g_opt_linear.load() != 0;
     const int wpc = waves_per_cu(c, cfg);
     const int items = job.item_base[np];
     long long blocks = g_opt_blocks.load();

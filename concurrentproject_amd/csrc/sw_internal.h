@@ -123,7 +123,8 @@ struct LaunchCfg {
     bool duo_f16 = false;   // MODE_DUO: max3 through v_pk_maximum3_f16 (every value < 0x7C00)
     bool f2_stream = false; // MODE_FLOW2: row codes streamed through per-wave LDS rings (rows too long to stage)
     int f2_wgs = 1;         // MODE_FLOW2 streamed: workgroups per CU (LDS pad sized to admit exactly this many)
-    bool f2_lin = false;    // MODE_FLOW2, C = 32: the linear-gap step (G_INIT == G_EXT, exact; sw_flow2.hip LIN)
+    bool f2_lin = false;    // G_INIT == G_EXT, the exact linear-gap step: MODE_FLOW2 at C = 32 (sw_flow2.hip
+                            // LIN) and MODE_DUO with duo_f16 (sw_kernels.hip StripDuo LIN)
 };
 constexpr int F2_WGS_AUTO = 2;   // flow2 streamed kernel, many groups per CU: workgroups per CU
 

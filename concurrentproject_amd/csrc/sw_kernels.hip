@@ -679,7 +679,10 @@ __device__ __forceinline__ DuoDesc load_duo(const KParams& kp, int idx) {
     return d;
 }
 
-template <int W, bool M3>
+// LIN (G_INIT == G_EXT, the reference's defaults): E+ = sat(H_left - G) and
+// F+ = sat(H_up - G) exactly (sw_flow2.hip, LIN), so a position keeps A and hg
+// only: 5.5 VALU per position and 5 per step instead of 9.5 and 7.
+template <int W, bool M3, bool LIN = false>
 struct StripDuo {
     unsigned pA[W], pB[W];                   // column penalty words: pair 0 (perm src1), pair 1 (perm src0)
     u16x2 aA[W], aB[W];                      // A = H + MATCH, ping-pong (diagonal source)
@@ -721,8 +724,46 @@ struct StripDuo {
     // move, and the code entering position 0 (lane l-1's position W-1, or the inflow
     // at lane 0) is written in place by the DPP that fetches it.
     template <int S>
+    __device__ __forceinline__ void step_lin(u16x2 (&aCur)[W], const u16x2 (&aPrev)[W], const u16x2 go2,
+                                             const u16x2 ma2, const u16x2 gom2) {
+        const u16x2 aL0 = as16((unsigned)dpp_shr1((int)IOA, (int)as32(aPrev[W - 1])));
+        constexpr int s0 = (W - S % W) % W;
+        r[s0] = (unsigned)dpp_shr1((int)IOR, (int)r[s0]);
+        const u16x2 hgL0 = vsubs2(aL0, gom2);
+        u16x2 tOdd = splat2(0);
+#pragma unroll
+        for (int p = W - 1; p >= 0; --p) {
+            const int q = p > 0 ? p - 1 : 0;
+            const u16x2 hgL = p > 0 ? hg[q] : hgL0;   // E+ = sat(H_left - G)
+            const unsigned rL = r[(p + W - S % W) % W];
+            const u16x2 aD = p > 0 ? aCur[q] : L0;
+            const u16x2 pen = as16(__builtin_amdgcn_perm(pB[p], pA[p], rL));
+            const u16x2 t = vsubs2(aD, pen);
+            u16x2 H;
+            if constexpr (M3) {
+                H = vmax3h(t, hgL, hg[p]);             // hg[p] (last step) = F+ = sat(H_up - G)
+                if constexpr (W == 1) M = vmax2(M, t);
+                else if (p & 1) tOdd = t;
+                else M = vmax3h(M, tOdd, t);
+            } else {
+                H = vmax2(vmax2(t, hgL), hg[p]);
+                M = vmax2(M, t);
+            }
+            aCur[p] = H + ma2;
+            hg[p] = vsubs2(H, go2);
+        }
+        L0 = aL0;
+        IOA = (unsigned)__builtin_amdgcn_update_dpp((int)as32(aCur[W - 1]), (int)IOA, DPP_WAVE_SHL1, 0xF, 0xF, false);
+        IOR = (unsigned)__builtin_amdgcn_mov_dpp((int)IOR, DPP_WAVE_SHL1, 0xF, 0xF, true);
+    }
+
+    template <int S>
     __device__ __forceinline__ void step(u16x2 (&aCur)[W], const u16x2 (&aPrev)[W], const u16x2 go2,
                                          const u16x2 ge2, const u16x2 ma2, const u16x2 gom2) {
+        if constexpr (LIN) {
+            step_lin<S>(aCur, aPrev, go2, ma2, gom2);
+            return;
+        }
         const u16x2 aL0 = as16((unsigned)dpp_shr1((int)IOA, (int)as32(aPrev[W - 1])));
         const u16x2 ehL0 = as16((unsigned)dpp_shr1((int)IOE, (int)as32(eh[W - 1])));
         constexpr int s0 = (W - S % W) % W;     // slot of position 0 (= last step's position W-1)
@@ -804,13 +845,13 @@ __device__ __forceinline__ unsigned codes_duo(unsigned raw0, unsigned raw1, int 
     return 0x0C000C00u | (s1 << 16) | s0;
 }
 
-template <int W, int C, bool M3>
+template <int W, int C, bool M3, bool LIN>
 __device__ void strip_pass_duo(const KParams& kp, const DuoDesc& d, const int strip, const int lane) {
     constexpr int SW = 64 * W;
     const int m = d.m_pad;
     const u16x2 go2 = splat2(kp.gap_init), ge2 = splat2(kp.gap_ext), ma2 = splat2(kp.match),
                 gom2 = splat2(kp.gap_init + kp.match);
-    StripDuo<W, M3> S;
+    StripDuo<W, M3, LIN> S;
     S.setup(kp, d, strip, lane);
     const bool has_in = strip > 0;
     const bool has_out = strip < d.strips - 1;
@@ -853,13 +894,13 @@ __device__ void strip_pass_duo(const KParams& kp, const DuoDesc& d, const int st
 // (12.43 vs 12.06 ms), so the step is issue-bound, not latency-bound.
 // M3: H = max3 and the running max fold two positions per v_pk_maximum3_f16
 // (scores below 0x7C00 only, LaunchCfg::duo_f16).
-template <int W, int C, bool M3>
+template <int W, int C, bool M3, bool LIN>
 __global__ void __launch_bounds__(64 * DUO_WAVES) sw_duo_kernel(KParams kp) {
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     for (int di = blockIdx.x; di < kp.npairs; di += gridDim.x) {
         const DuoDesc d = load_duo(kp, di);
-        for (int strip = wave; strip < d.strips; strip += DUO_WAVES) strip_pass_duo<W, C, M3>(kp, d, strip, lane);
+        for (int strip = wave; strip < d.strips; strip += DUO_WAVES) strip_pass_duo<W, C, M3, LIN>(kp, d, strip, lane);
     }
 }
 
@@ -890,8 +931,13 @@ hipError_t launch_t(const LaunchCfg& cfg, const KParams& kp, hipStream_t s) {
             return hipErrorInvalidValue;
         case MODE_DUO:
             if constexpr (DNA) {
-                if (cfg.duo_f16) hipLaunchKernelGGL((sw_duo_kernel<W, C, true>), dim3(cfg.blocks), dim3(64 * DUO_WAVES), 0, s, kp);
-                else hipLaunchKernelGGL((sw_duo_kernel<W, C, false>), dim3(cfg.blocks), dim3(64 * DUO_WAVES), 0, s, kp);
+                // the linear-gap step (G_INIT == G_EXT) is built with the f16-max3 form
+                if (cfg.duo_f16 && cfg.f2_lin)
+                    hipLaunchKernelGGL((sw_duo_kernel<W, C, true, true>), dim3(cfg.blocks), dim3(64 * DUO_WAVES), 0, s, kp);
+                else if (cfg.duo_f16)
+                    hipLaunchKernelGGL((sw_duo_kernel<W, C, true, false>), dim3(cfg.blocks), dim3(64 * DUO_WAVES), 0, s, kp);
+                else
+                    hipLaunchKernelGGL((sw_duo_kernel<W, C, false, false>), dim3(cfg.blocks), dim3(64 * DUO_WAVES), 0, s, kp);
                 break;
             }
             return hipErrorInvalidValue;
@@ -910,7 +956,7 @@ int waves_t(int mode) {
             if constexpr (DNA) return occupancy_waves(sw_flow_kernel<W, C>);
             return 0;
         case MODE_DUO:
-            if constexpr (DNA) return occupancy_waves(sw_duo_kernel<W, C, true>, 64 * DUO_WAVES);
+            if constexpr (DNA) return occupancy_waves(sw_duo_kernel<W, C, true, false>, 64 * DUO_WAVES);
             return 4;
         default: return 4;
     }

@@ -124,6 +124,13 @@ def test_config_c3_batch_1024(engine, golden):
     N = c["N"]
     pairs = [(arena[2 * N * k:2 * N * k + N], arena[2 * N * k + N:2 * N * (k + 1)]) for k in range(c["npairs"])]
     assert engine.score_batch(pairs) == c["scores"]
+    assert engine.last_stats()["variant"] & 8          # the linear-gap duo step (G_INIT == G_EXT)
+    engine.set_option("linear", 0)                     # and the affine duo step
+    try:
+        assert engine.score_batch(pairs) == c["scores"]
+        assert not engine.last_stats()["variant"] & 8
+    finally:
+        engine.set_option("linear", -1)
 
 
 def test_config_c4_batch_8192_device(engine, golden):
@@ -350,7 +357,10 @@ def test_duo_batches(engine, oracle_mod):
     """Packed 16-bit duo kernel: odd batch sizes, ragged shapes padded inside a
     duo, several constants; chosen automatically for DNA batches."""
     rng = np.random.default_rng(77)
-    for prm in (engine.Params(), engine.Params(2, -3, 5, 2), engine.Params(3, -1, 4, 1)):
+    for prm, lin in ((engine.Params(), -1), (engine.Params(), 0), (engine.Params(2, -3, 5, 2), -1),
+                     (engine.Params(3, -1, 4, 1), -1), (engine.Params(3, -2, 5, 5), -1)):
+        # G_INIT == G_EXT: the exact linear-gap duo step unless linear = 0
+        engine.set_option("linear", lin)
         op = oracle_mod.Params(prm.match, prm.mismatch, prm.gap_init, prm.gap_ext)
         for npairs in (1, 2, 3, 7):
             pairs = []
@@ -363,9 +373,12 @@ def test_duo_batches(engine, oracle_mod):
                 pairs.append((a, b))
             exp = [oracle_mod.score_linear(a, b, op) for a, b in pairs]
             engine.set_option("mode", 3)
-            assert engine.score_batch(pairs, prm) == exp, (prm, npairs)
+            assert engine.score_batch(pairs, prm) == exp, (prm, npairs, lin)
+            st = engine.last_stats()
+            assert bool(st["variant"] & 8) == (lin == -1 and prm.gap_init == prm.gap_ext and st["variant"] & 1), st
             engine.set_option("mode", -1)
-            assert engine.score_batch(pairs, prm) == exp, (prm, npairs)
+            assert engine.score_batch(pairs, prm) == exp, (prm, npairs, lin)
+    engine.set_option("linear", -1)
 
 
 def test_duo_f16_max3_boundary(engine, oracle_mod):
