@@ -3,6 +3,7 @@ declares.  Only host-side entry points are called (no GPU here)."""
 import ctypes
 import os
 import re
+import sys
 
 import numpy as np
 import pytest
@@ -112,3 +113,41 @@ def test_no_oracle_in_product():
             if f.endswith((".py", ".hip", ".cpp", ".h")):
                 txt = open(os.path.join(dp, f)).read()
                 assert "import oracle" not in txt and "sworacle" not in txt, f
+
+
+def test_slab_edges_are_system_scope():
+    """Cross-GPU slab edges are loaded and stored system scope (sc0 sc1: the LLVM
+    memory model's relaxed system-scope atomic on gfx950); in-GPU edges device
+    scope (sc1 only).  Checked on the built code object's disassembly (the
+    flow2 kernel template <C, STREAM, RING, SLAB, LIN>, sw_flow2.hip)."""
+    import re
+    import tempfile
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import codeobj
+    lib = os.path.join(ROOT, "concurrentproject_amd", "libswmi355.so")
+    if not os.path.exists(lib):
+        pytest.skip("library not built")
+    funcs = {}
+    with tempfile.TemporaryDirectory() as d:
+        for text in codeobj.disassemble(lib, d):
+            funcs.update(codeobj.functions(text))
+    pat = re.compile(r"sw_flow2_kernelILi(\d+)ELb(\d)ELb(\d)ELb(\d)ELb(\d)E")
+    seen = {0: 0, 1: 0}
+    for name, body in funcs.items():
+        m = pat.search(name)
+        if not m:
+            continue
+        slab = int(m.group(4))
+        seen[slab] += 1
+        g_loads = [x for x in body if x.startswith("buffer_load_dwordx4")]
+        g_stores = [x for x in body if x.startswith("buffer_store_dwordx4")]
+        assert g_loads and g_stores, name
+        sys_ops = [x for x in g_loads + g_stores if "sc0 sc1" in x]
+        if slab:
+            # the peer in- and outflow loops: system-scope loads and stores
+            assert any(x.startswith("buffer_load") for x in sys_ops), name
+            assert any(x.startswith("buffer_store") for x in sys_ops), name
+        else:
+            assert not sys_ops, (name, sys_ops[:3])
+            assert all(" sc1" in x for x in g_stores), name
+    assert seen[0] >= 6 and seen[1] >= 3, seen
