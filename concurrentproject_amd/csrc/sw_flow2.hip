@@ -48,7 +48,7 @@ constexpr int F2_R = 256;   // ring rows per link (power of two, >= 2C + 64)
 #define SW_F2_SPEC 0        // >0: the next chunk's inflow is read speculatively after SW_F2_SPEC/4 of a chunk
 #endif
 #ifndef SW_F2_GPOS
-#define SW_F2_GPOS 2        // chunk c+SW_F2_GPREF's granules are loaded after SW_F2_GPOS/4 of chunk c's steps
+#define SW_F2_GPOS 1        // chunk c+SW_F2_GPREF's granules are loaded after SW_F2_GPOS/4 of chunk c's steps
 #endif
 #ifndef SW_F2_HALFPUB
 #define SW_F2_HALFPUB 1     // workgroup-edge strips publish granules every half chunk

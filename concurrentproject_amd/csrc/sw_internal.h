@@ -110,7 +110,10 @@ constexpr int RING_CONS_STRIDE = 32;   // dwords between consumer progress words
 enum : int { MODE_STRIP = 0, MODE_PAIRWG = 1, MODE_CHAIN = 2, MODE_DUO = 3, MODE_FLOW = 4, MODE_FLOW2 = 5 };
 inline bool grouped_mode(int mode) { return mode == MODE_CHAIN || mode == MODE_FLOW || mode == MODE_FLOW2; }
 
-constexpr int DUO_WAVES = 4;   // waves per workgroup of the duo kernel (one workgroup per duo; 8 measured slower)
+#ifndef SW_DUO_WAVES
+#define SW_DUO_WAVES 4
+#endif
+constexpr int DUO_WAVES = SW_DUO_WAVES;   // waves per workgroup of the duo kernel (one workgroup per duo)
 
 // Host-side launch (sw_kernels.hip).
 struct LaunchCfg {
