@@ -56,18 +56,19 @@ def run(engine: str, threads: int) -> None:
 
 
 def merge() -> None:
-    r = json.load(open(os.path.join(HERE, "c5_ref.json")))
-    w = json.load(open(os.path.join(HERE, "c5_wavefront.json")))
-    assert r["sha256"] == w["sha256"], "different pairs"
-    assert r["score"] == w["score"], (r["score"], w["score"])
+    """configs.json["C5"] from every engine result present; all must agree."""
+    res = [json.load(open(os.path.join(HERE, "c5_%s.json" % e))) for e in ("ref", "wavefront")
+           if os.path.exists(os.path.join(HERE, "c5_%s.json" % e))]
+    assert res, "no C5 result yet"
+    assert len({r["sha256"] for r in res}) == 1, "different pairs"
+    assert len({r["score"] for r in res}) == 1, [r["score"] for r in res]
     path = os.path.join(HERE, "configs.json")
     cfg = json.load(open(path))
-    cfg["C5"] = {"seed": SEED, "N": N, "score": r["score"], "sha256": r["sha256"],
-                 "pinned_by": [r["source"] + " in %.0f s" % r["seconds"],
-                               w["source"] + " in %.0f s" % w["seconds"]]}
+    cfg["C5"] = {"seed": SEED, "N": N, "score": res[0]["score"], "sha256": res[0]["sha256"],
+                 "pinned_by": [r["source"] + " in %.0f s" % r["seconds"] for r in res]}
     with open(path, "w") as f:
-        json.dump(cfg, f)
-    print("C5", r["score"])
+        json.dump(cfg, f, indent=1)
+    print("C5", res[0]["score"], cfg["C5"]["pinned_by"])
 
 
 if __name__ == "__main__":

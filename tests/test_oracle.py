@@ -138,3 +138,12 @@ def test_restatement_vs_reference_long_affine(oracle_mod):
                     np.concatenate([b[:cut], a[:ln], b[cut:]])[:m]
             exp = oracle_mod.ref_score(a, b, prm, which="lazy")
             assert oracle_mod.score_linear(a, b, prm) == exp == oracle_mod.ref_score(a, b, prm), (prm, n, m)
+
+
+def test_config_c5_fixture(oracle_mod, golden):
+    """The C5 golden (N = 2^20, seed 1048576) belongs to the generator's pair and
+    names the engines that computed it (tests/golden/gen_c5.py)."""
+    c = golden("configs.json")["C5"]
+    a, b = oracle_mod.gen_pair(c["seed"], c["N"])
+    assert _sha(a, b) == c["sha256"]
+    assert c["score"] == 119470 and c["pinned_by"]
