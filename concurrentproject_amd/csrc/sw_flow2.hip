@@ -92,7 +92,7 @@ __device__ __forceinline__ int sbyte(unsigned w) {
 // codes, each wave keeps its own ring of F2_CR row codes in LDS -- row r in slot
 // (r + 64) mod F2_CR, slots [0, C) mirrored behind the ring so that a lane's
 // unaligned 4-row read never wraps -- and refills it one chunk ahead: C lanes load
-// the raw bytes of chunk c+4 (buffer_load_ubyte, two chunks of latency cover) and
+// the raw bytes of chunk c+3 (buffer_load_ubyte, one chunk of latency cover) and
 // store the codes of chunk c+2 (two ds_write_b8).  The step loop is unchanged.
 constexpr int F2_CR = 256;
 
@@ -228,14 +228,16 @@ __global__ void __launch_bounds__(256) sw_flow2_kernel(KParams kp) {
             if constexpr (STREAM) return cr + ((k0 + 64 - lane) & (F2_CR - 1));
             else return code_base + k0;
         };
-        unsigned rq0 = 0, rq1 = 0;   // STREAM: raw bytes of chunks c+2, c+3 in flight
+        // STREAM: the raw bytes of chunk c+2, loaded during chunk c-1: one register
+        // instead of a rotated pair (copying an in-flight load's destination makes the
+        // compiler wait for that load; C5 430 -> 422 ms)
+        unsigned rq0 = 0;
         if constexpr (STREAM) {
             for (int i = lane; i < CRB / 4; i += 64) reinterpret_cast<unsigned*>(cr)[i] = 0u;   // rows < 0: no row
             const unsigned r0 = raw_of(0), r1 = raw_of(1);
             put_codes(r0, 0);
             put_codes(r1, 1);
             rq0 = raw_of(2);
-            rq1 = raw_of(3);
         }
 
         auto flow_loop = [&](auto in_c, auto out_c) __attribute__((always_inline)) {
@@ -399,10 +401,9 @@ __global__ void __launch_bounds__(256) sw_flow2_kernel(KParams kp) {
 #ifdef SW_TIMELINE
                 if (c == 0) t_first = realtime_waited();
 #endif
-                if constexpr (STREAM) {   // refill the ring: codes of chunk c+2, raw bytes of chunk c+4
+                if constexpr (STREAM) {   // refill the ring: codes of chunk c+2, raw bytes of chunk c+3
                     put_codes(rq0, c + 2);
-                    rq0 = rq1;
-                    rq1 = raw_of(c + 4);
+                    rq0 = raw_of(c + 3);
                 }
 #pragma unroll
                 for (int u = 0; u < C / 4; ++u) D[u] = load_u32_unaligned(code_at(k0 + C) + 4 * u);
