@@ -404,6 +404,21 @@ def main():
                 parity = "ok" if first == gold["C2"]["score"] else "MISMATCH"
             elif workload == "slab" and N == 1 << 20 and slab_buf is None and "C5" in gold:
                 parity = "ok" if first == gold["C5"]["score"] else "MISMATCH"
+        # N=1: the general affine step on the same pair (the automatic plan takes the
+        # exact linear-gap step at G_INIT == G_EXT), for reference
+        affine = None
+        if workload == "pair" and world == 1 and args.workload == "auto" and not args.no_extra and \
+                params[2] == params[3]:
+            sw.set_option("linear", 0)
+            try:
+                at, ak = time_launches(torch, launch, lambda: None, max(3, args.steps // 2), 1, stream, None)
+                sw.stream_status(sptr)
+                ok = ("ok" if scores[0].item() == gold.get("C2", {}).get("score") else "MISMATCH") \
+                    if defaults and N == 65536 else "unchecked"
+                affine = {"kernel_ms_per_launch": round(ak, 4), "kernel_gcups": round(N * N / (ak * 1e-3) / 1e9, 3),
+                          "parity": ok, "note": "option linear=0: the general affine (E, F) step on the C2 pair"}
+            finally:
+                sw.set_option("linear", -1)
         # N=1: the batched config (C3) measured right after, as an extra key
         if workload == "pair" and world == 1 and args.workload == "auto" and not args.no_extra:
             bt, bk, bsc, bcells, bst = run_batch(sw, torch, None, 1, 0, 8192, 1024, max(3, args.steps // 2), 1)
@@ -416,6 +431,16 @@ def main():
                      "kernel": {3: "duo", 1: "pairwg"}.get(bst["mode"], bst["mode"]),
                      "dtype": "u16x2 (packed, exact: scores < 2^16)" if bst["mode"] == 3 else "int32",
                      "roofline": roofline("batch", bcells, bk)}
+            # the same batch on the int32 pair-per-workgroup kernel (no 16-bit packing)
+            sw.set_option("mode", 1)
+            try:
+                it, ik, isc, _, ist = run_batch(sw, torch, None, 1, 0, 8192, 1024, 2, 1)
+                extra["int32_kernel"] = {"kernel": "pairwg", "kernel_ms_per_launch": round(ik, 4),
+                                         "kernel_gcups": round(bcells / (ik * 1e-3) / 1e9, 3),
+                                         "parity": ("ok" if isc == ref[:len(isc)] else "MISMATCH")
+                                         if defaults and len(ref) >= 1024 else "unchecked"}
+            finally:
+                sw.set_option("mode", args.mode if args.mode >= 0 else -1)
 
     value = cells_job * args.steps / t_max / 1e9
     if rank == 0:
@@ -445,6 +470,8 @@ def main():
         }
         if extra is not None:
             out["batch_c3"] = extra
+        if workload != "batch" and affine is not None:
+            out["affine_step"] = affine
         if world == 1 and not args.no_cpu_baseline:
             try:
                 out["cpu_baseline"] = cpu_baseline(workload, cfg["N"], args.cpu_seconds, params)
