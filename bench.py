@@ -157,8 +157,10 @@ def profile_for(workload):
         prof = json.load(open(path))
     except Exception as e:
         return None, repr(e)
-    if prof.get("lib_sha256") != lib_sha256(sw.LIB_PATH):
-        return None, "stale: profile taken with another libswmi355.so build"
+    # the profile's kernels must be this build's: same library file, or (after a
+    # rebuild) the same engine sources and flags
+    if prof.get("lib_sha256") != lib_sha256(sw.LIB_PATH) and prof.get("source_sha256") != sw.source_stamp():
+        return None, "stale: profile taken with another build of the engine"
     return prof, os.path.relpath(path, ROOT)
 
 

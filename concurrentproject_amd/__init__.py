@@ -65,6 +65,22 @@ def build(verbose: bool = False) -> str:
     return LIB_PATH
 
 
+def source_stamp() -> str:
+    """sha256 over the engine's sources and build flags (csrc/*.hip, *.h, Makefile and
+    include/algoGPU.h): identifies the kernels a profile was taken with, across rebuilds."""
+    import glob
+    import hashlib
+    h = hashlib.sha256()
+    csrc = os.path.join(HERE, "csrc")
+    files = sorted(glob.glob(os.path.join(csrc, "*.hip")) + glob.glob(os.path.join(csrc, "*.h")) +
+                   [os.path.join(csrc, "Makefile"), os.path.join(HERE, "..", "include", "algoGPU.h")])
+    for f in files:
+        h.update(os.path.basename(f).encode())
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()
+
+
 def lib() -> ctypes.CDLL:
     """The loaded engine.  Raises if libswmi355.so has not been built (no fallback)."""
     global _lib

@@ -54,6 +54,12 @@ def per_launch(path, counter=None):
     return k, sum(vals) / len(vals), len(vals)
 
 
+def source_stamp():
+    sys.path.insert(0, ROOT)
+    import concurrentproject_amd as sw
+    return sw.source_stamp()
+
+
 def sha256(path):
     h = hashlib.sha256()
     with open(path, "rb") as f:
@@ -76,7 +82,8 @@ def main():
         k = _engine_kernel(_rows(stats), key="Name")
         st = [r for r in _rows(stats) if r["Name"] == k][0]
         t_ns = float(st["AverageNs"])
-        out = {"kernel": k, "lib_sha256": sha256(LIB), "kernel_avg_ns": t_ns, "kernel_calls": int(st["Calls"]),
+        out = {"kernel": k, "lib_sha256": sha256(LIB), "source_sha256": source_stamp(), "kernel_avg_ns": t_ns,
+               "kernel_calls": int(st["Calls"]),
                "algorithmic_bytes_per_launch": CELLS[cfg] * ALGO_BYTES_PER_CELL, "cells_per_launch": CELLS[cfg]}
         passes = []
         fetch = os.path.join(src, "fetch_" + cfg, cfg + "_counter_collection.csv")
