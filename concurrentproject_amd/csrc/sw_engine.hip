@@ -516,9 +516,9 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
     // (4162 groups; fine on 794), consistent with not every block being resident,
     // which the deal needs -- and the gain measured with linear edges was 9 %.
     int f2_wgs = 1;
-    if (f2s && !job.ring) {
+    if (f2s) {
         const long long o = g_opt_f2_wgs.load();
-        f2_wgs = o > 0 ? (int)o : (job.item_base[np] >= 8 * c->cus ? F2_WGS_AUTO : 1);
+        f2_wgs = o > 0 ? (int)o : (!job.ring && job.item_base[np] >= 8 * c->cus ? F2_WGS_AUTO : 1);
     }
     int ring_blocks = 0, wrap_rows = 0;
     if (job.ring) {

@@ -193,6 +193,7 @@ __global__ void __launch_bounds__(256) sw_flow2_kernel(KParams kp) {
         bool failed = false;
         long long t_first = t_start;
         int nslow = 0;   // chunks whose inflow took the slow path (trace only)
+        int fail_in = -1, fail_bp = -1;   // RING trace: chunk whose inflow / back-pressure wait timed out
         long long tl[5] = {0, 0, 0, 0, 0};   // SW_TIMELINE: wall clock at chunks 1, 2, 3, 50, 1000
         int H = 0, E = 0, fh = -ge, hgO = -go, L0 = -go, ehP = -ge, M = 0;
         int IOH = -go, IOE = -ge;                 // rotating I/O registers (see the step)
@@ -274,6 +275,7 @@ __global__ void __launch_bounds__(256) sw_flow2_kernel(KParams kp) {
                                 __hip_atomic_load(bp_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
                             if ((long long)__builtin_amdgcn_s_memrealtime() - t_start > kp.timeout_ticks) {
                                 failed = true;
+                                if (fail_bp < 0) fail_bp = k0;
                                 break;
                             }
                         }
@@ -322,6 +324,9 @@ __global__ void __launch_bounds__(256) sw_flow2_kernel(KParams kp) {
                         nslow += __all((!need) | granule_ok(g, in_e, row)) ? 0 : 1;
                     }
                     await_granules<C, AIN>(kp, in_e, g, k0, lane, m, strip, failed);
+                    if constexpr (RING) {
+                        if (kp.trace != nullptr && failed && fail_in < 0) fail_in = k0;
+                    }
                     // ring mode: rows < k0 + C are consumed (reported every 4th chunk and at
                     // the last).  An unconditional store, dropped (offset OOR) where there is
                     // nothing to report: no branch around a memory op in the chunk loop.
@@ -474,6 +479,8 @@ __global__ void __launch_bounds__(256) sw_flow2_kernel(KParams kp) {
             t[0] = (unsigned long long)t_start;
             t[1] = (unsigned long long)t_first;
             t[3] = (unsigned long long)nslow;
+            t[4] = (unsigned long long)(long long)fail_in;
+            t[5] = (unsigned long long)(long long)fail_bp;
             t[2] = (unsigned long long)__builtin_amdgcn_s_memrealtime();
             t[7] = (unsigned long long)nloc;
             for (int q = 0; q < 5; ++q) t[8 + q] = (unsigned long long)tl[q];

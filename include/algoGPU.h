@@ -159,6 +159,14 @@ void sw_db_close(sw_db* db);
  *              4 = free-running strip groups, rows staged in LDS (long DNA pairs)
  *   "duo16"    1 = (default) packed duos take max3 through v_pk_maximum3_f16 when every
  *              value stays below 0x7C00 (MATCH*(min(n,m)+1) <= 31743), 0 = u16 max only
+ *   "linear"   -1 = (default) the exact linear-gap step when G_INIT == G_EXT
+ *              (flow2 C = 32, f16 duos), 0 = always the affine step
+ *   "ring"     -1 = (default) ring edges for a single flow2 pair whose linear edges
+ *              would exceed 1 GB, 0 = never, 1 = always (one pair per launch)
+ *   "ring_rows" rows per within-round ring, a power of two in [512, 2^20] (4096)
+ *   "f2_wgs"   flow2 streamed kernel: workgroups per CU, 0 = auto, 1..4
+ *   "f2stream" 1 = flow2 streams the row codes even when they fit in LDS (tests)
+ *   "trace"    device address of a 16 x u64 per-strip trace buffer, 0 = off (tools)
  * Returns 0, or -1 for an unknown key / bad value. */
 int sw_set_option(const char* key, long long value);
 long long sw_get_option(const char* key);
@@ -171,7 +179,8 @@ typedef struct {
     int W, C, dna, blocks, waves_per_cu, items;
     long long boundary_bytes;
     int mode;
-    int variant;            /* bit 0: duo max3 via v_pk_maximum3_f16; bit 1: flow2 streams row codes */
+    int variant;            /* bit 0: duo max3 via v_pk_maximum3_f16; bit 1: flow2 streams row codes;
+                               bit 2: flow2 ring edges; bit 3: the linear-gap step */
 } sw_stats;
 int sw_last_stats(sw_stats* out);
 

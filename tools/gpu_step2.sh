@@ -1,5 +1,4 @@
 set -e
-rm -rf gpurun_out/ab gpurun_out/ab2
-bash tools/ab_multi.sh "libswmi355 libswmi355_DW8" --workload batch --steps 5 --warmup 1
-mv gpurun_out/ab gpurun_out/ab2
-bash tools/ab_multi.sh "libswmi355 libswmi355_DW8" --workload batch --steps 5 --warmup 1 --W 4
+mkdir -p gpurun_out/pr
+timeout -k 10 100 python tools/probe_ring.py 400000 2 5 > gpurun_out/pr/a.txt 2>&1
+timeout -k 10 100 python tools/probe_ring.py 1048576 2 5 > gpurun_out/pr/b.txt 2>&1
