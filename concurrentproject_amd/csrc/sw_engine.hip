@@ -512,13 +512,17 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
     // with many strip groups per CU (C5) is throughput-bound, and more waves per
     // SIMD hide each other's issue latency (sw_flow2.hip launch_c sizes the LDS pad)
     const bool f2s = job.mode == MODE_FLOW2 && (job.f2_stream || job.ring || edge != nullptr);
-    // Ring mode keeps one per CU: at 2 or 3 per CU its static deal timed out on C5
-    // (4162 groups; fine on 794), consistent with not every block being resident,
-    // which the deal needs -- and the gain measured with linear edges was 9 %.
+    // Measured (kernel ms, ring | linear edges, 1/2/3/4 per CU):
+    //   N = 2^17 (520 groups)   9.8 9.7 9.6 9.6   | 9.4 10.8 12.5 12.8
+    //   N = 2^18 (1040)         32.4 25.2 26.2 26.4 | 31.7 26.3 34.2 32.1
+    //   N = 2^19 (2080)         116 83.9 80.1 78.9  | 117 83.2 88.5 96.2
+    //   N = 2^20 (4162, C5)     437 312 287 283     | 454 307 299 -
+    // ring: one per 2 CUs' worth of groups, up to 4; linear edges: 2 from 4 groups per CU
     int f2_wgs = 1;
     if (f2s) {
         const long long o = g_opt_f2_wgs.load();
-        f2_wgs = o > 0 ? (int)o : (!job.ring && job.item_base[np] >= 8 * c->cus ? F2_WGS_AUTO : 1);
+        const int per_cu = job.item_base[np] / c->cus;
+        f2_wgs = o > 0 ? (int)o : job.ring ? std::min(F2_WGS_MAX, std::max(1, per_cu / 2)) : per_cu >= 4 ? 2 : 1;
     }
     int ring_blocks = 0, wrap_rows = 0;
     if (job.ring) {

@@ -263,8 +263,12 @@ __global__ void __launch_bounds__(256) sw_flow2_kernel(KParams kp) {
                 const int row_out = k0 - 128 + lane;
                 constexpr int LO = SW_F2_HALFPUB ? 64 - C / 2 : 64 - C;
                 const bool st = lane >= LO && row_out >= 0 && row_out < m;
-                if (RING && bp_word != nullptr && k0 - 64 > kp.ring_rows) {
-                    // rows <= k0 - 65 go out: positions <= pos0 + k0 - 65 - R must be consumed
+                if (RING && bp_word != nullptr) {
+                    // rows <= k0 - 65 go out: positions <= pos0 + k0 - 65 - R must be consumed.
+                    // Also at the start of a round (k0 - 64 <= R): the slots then still hold the
+                    // previous round's last rows, which the consumer (one hop behind, in that
+                    // round) may not have read yet; `need` is then below pos0, in wrap-safe
+                    // unsigned arithmetic, and in round 0 below 0, so always met.
                     const unsigned need = out_e.pos0 + (unsigned)(k0 - 64 - kp.ring_rows);
                     if ((int)(bp_seen - need) < 0) {
                         bp_seen = __builtin_amdgcn_readfirstlane(
@@ -479,8 +483,8 @@ __global__ void __launch_bounds__(256) sw_flow2_kernel(KParams kp) {
             t[0] = (unsigned long long)t_start;
             t[1] = (unsigned long long)t_first;
             t[3] = (unsigned long long)nslow;
-            t[4] = (unsigned long long)(long long)fail_in;
-            t[5] = (unsigned long long)(long long)fail_bp;
+            t[13] = (unsigned long long)(long long)fail_in;
+            t[14] = (unsigned long long)(long long)fail_bp;
             t[2] = (unsigned long long)__builtin_amdgcn_s_memrealtime();
             t[7] = (unsigned long long)nloc;
             for (int q = 0; q < 5; ++q) t[8 + q] = (unsigned long long)tl[q];

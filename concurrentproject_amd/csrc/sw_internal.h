@@ -129,7 +129,7 @@ struct LaunchCfg {
     bool f2_lin = false;    // G_INIT == G_EXT, the exact linear-gap step: MODE_FLOW2 at C = 32 (sw_flow2.hip
                             // LIN) and MODE_DUO with duo_f16 (sw_kernels.hip StripDuo LIN)
 };
-constexpr int F2_WGS_AUTO = 2;   // flow2 streamed kernel, many groups per CU: workgroups per CU
+constexpr int F2_WGS_MAX = 4;   // flow2 streamed kernel: most workgroups per CU (launch_c sizes the LDS pad)
 
 // MODE_FLOW stages a pair's row codes in LDS: one byte per row plus the
 // prefetch tail; pairs whose rows do not fit use MODE_CHAIN.

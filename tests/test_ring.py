@@ -7,7 +7,7 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 ACGT = np.frombuffer(b"ACGT", np.uint8)
-OPTS = ("W", "C", "blocks", "orient", "f2stream")
+OPTS = ("W", "C", "blocks", "orient", "f2stream", "f2_wgs")
 
 
 @pytest.fixture(autouse=True)
@@ -74,6 +74,26 @@ def test_ring_matches_linear_edges(engine):
     assert engine.score(a, b) == lin
     st = engine.last_stats()
     assert st["variant"] & 4 and st["boundary_bytes"] < 64 << 20, st
+
+
+@pytest.mark.parametrize("wgs", [1, 2, 3, 4])
+def test_ring_round_change(engine, wgs):
+    """1588 groups over 256..1024 resident blocks (2..7 rounds): a block starts its
+    next round while the consumer of its ring, one hop behind, still reads the last
+    rows of the previous one.  The back-pressure check also covers a round's first
+    R rows (before it did not, and N = 400000 at 2 workgroups per CU timed out).
+    Ring edges at 1..4 workgroups per CU against write-once edges."""
+    a, b = engine.gen_pair(400000, 400000)
+    engine.set_option("f2_wgs", wgs)
+    engine.set_option("ring", 0)
+    lin = engine.score(a, b)
+    engine.set_option("ring", 1)
+    got = engine.score(a, b)
+    st = engine.last_stats()
+    import torch
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    assert st["variant"] & 4 and st["blocks"] == min(1588, wgs * cus), st
+    assert got == lin > 0, (got, lin)
 
 
 def test_config_c5_golden(engine, golden):

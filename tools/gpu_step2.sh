@@ -1,4 +1,4 @@
 set -e
 mkdir -p gpurun_out/pr
-timeout -k 10 100 python tools/probe_ring.py 400000 2 5 > gpurun_out/pr/a.txt 2>&1
-timeout -k 10 100 python tools/probe_ring.py 1048576 2 5 > gpurun_out/pr/b.txt 2>&1
+timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_ring.py > gpurun_out/pr/ring.txt 2>&1
+timeout -k 10 120 python bench.py --workload slab --steps 3 --warmup 1 --no-cpu-baseline --no-extra > gpurun_out/pr/bench_c5.txt 2>&1

@@ -45,6 +45,11 @@ start = (tr[:, 0] - t0) / 1e5   # ms
 end = (tr[:, 2] - t0) / 1e5
 dur = end - start
 groups = strips // 4
+never = np.where(tr[:, 0] == 0)[0]
+print("strips never traced:", len(never), "first groups", sorted(set((never // 4).tolist()))[:16])
+g0 = start[0:4 * min(groups, st["blocks"]):4]
+late = np.where(g0 > 0.5)[0]
+print("round-0 groups starting after 0.5 ms:", len(late), late[:16].tolist(), np.round(g0[late[:16]], 2).tolist())
 if err is not None:
     slow = np.where(dur > 0.5 * float(sys.argv[3] if len(sys.argv) > 3 else 5) * 1e3)[0]
     print("strips over half the time-out:", len(slow), "first", slow[:12].tolist())
@@ -53,15 +58,15 @@ if err is not None:
         for k in first:
             g = k // 4
             print(" strip", k, "group", g, "block", g % st["blocks"], "round", g // st["blocks"],
-                  "start %.2f end %.2f" % (start[k], end[k]), "fail_in", tr[k, 4], "fail_bp", tr[k, 5])
-    fi = np.where((tr[:, 4] >= 0) | (tr[:, 5] >= 0))[0]
+                  "start %.2f end %.2f" % (start[k], end[k]), "fail_in", tr[k, 13], "fail_bp", tr[k, 14])
+    fi = np.where(((tr[:, 13] >= 0) | (tr[:, 14] >= 0)) & (tr[:, 0] > 0))[0]
     print("strips with a recorded failure:", len(fi))
     for k in fi[:16]:
-        print(" strip", k, "group", k // 4, "fail_in", tr[k, 4], "fail_bp", tr[k, 5],
+        print(" strip", k, "group", k // 4, "fail_in", tr[k, 13], "fail_bp", tr[k, 14],
               "start %.2f end %.2f" % (start[k], end[k]))
     lo = max(0, fi[0] // 4 - 2) * 4 if len(fi) else 0
     for k in range(lo, lo + 20):
-        print(" ctx strip", k, "start %.2f end %.2f dur %.2f" % (start[k], end[k], dur[k]), "fail_in", tr[k, 4],
-              "fail_bp", tr[k, 5])
+        print(" ctx strip", k, "start %.2f end %.2f dur %.2f" % (start[k], end[k], dur[k]), "fail_in", tr[k, 13],
+              "fail_bp", tr[k, 14])
 else:
     print("max strip duration ms %.2f" % dur.max())

@@ -1,5 +1,7 @@
-"""Probe: flow2 streamed kernel at several workgroups per CU, ring and linear edges
-(diagnostic for a hang seen at f2_wgs=2 on C5)."""
+"""Probe: flow2 streamed kernel at several workgroups per CU, ring and linear edges;
+kernel time of the second of two runs.
+
+    python tools/probe_wgs.py N [rings] [wgs list] [timeout_s]"""
 import os, sys, time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np
@@ -22,10 +24,11 @@ for ring in RINGS:
         sw.set_option("f2stream", 1)
         t = time.time()
         try:
-            sw.score_batch_device(arena.data_ptr(), [0], [N], [N], [N], score.data_ptr(), flags=1, stream=s)
-            sw.stream_status(s)
+            for _ in range(2):
+                sw.score_batch_device(arena.data_ptr(), [0], [N], [N], [N], score.data_ptr(), flags=1, stream=s)
+                sw.stream_status(s)
             st = sw.last_stats()
-            print("ring", ring, "wgs", w, "score", score.item(), "ms %.1f" % ((time.time() - t) * 1e3), "blocks", st["blocks"],
-                  "variant", st["variant"], flush=True)
+            print("N", N, "ring", ring, "wgs", w, "score", score.item(), "kernel_ms %.2f" % st["kernel_ms"],
+                  "blocks", st["blocks"], "variant", st["variant"], "edge_MB %.1f" % (st["boundary_bytes"] / 1e6), flush=True)
         except Exception as e:
             print("ring", ring, "wgs", w, "ERROR", e, "s %.1f" % (time.time() - t), flush=True)
