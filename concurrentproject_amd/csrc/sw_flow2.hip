@@ -65,6 +65,15 @@ __device__ __forceinline__ int dpp_add_shr1_tied(int old, int src, int k, int af
         : "+v"(old) : "v"(src), "v"(k), "v"(after));
     return old;
 }
+// The same with t0 = max(t, 0) computed inside, between the write of src and the
+// DPP read of it: `after` may then be the instruction right behind the one that
+// writes src, and the second wait state of the hazard is a useful instruction
+// (an s_nop there cost the C2 kernel 5 %).
+__device__ __forceinline__ int dpp_add_shr1_tied_max0(int old, int src, int k, int after, int t, int& t0) {
+    asm("v_max_i32_e32 %1, 0, %4\n\tv_add_u32_dpp %0, %2, %3 wave_shr:1 row_mask:0xf bank_mask:0xf ; dep %5"
+        : "+v"(old), "=&v"(t0) : "v"(src), "v"(k), "v"(t), "v"(after));
+    return old;
+}
 
 // s_memrealtime with its wait inside the asm: nothing SMEM stays outstanding, so
 // the compiler's LDS wait counts around a stamp stay exact (tools only)
@@ -106,10 +115,11 @@ constexpr int F2_CR = 256;
 // E(i,j-1) <= H(i,j-1) (H is a max over E), so max(E(i,j-1) - G, H(i,j-1) - G)
 // is the second term; the same for F.  The step keeps H only:
 //   t   = H(i-1,j-1) + s            (SDWA add, as above)
-//   hgL = wave_shr1(hgO)            lanes 1..63: H(i,j-1) - G; lane 0 the inflow row
-//   H   = max(max3(hgL, hgO, 0), t) hgO = H(i-1,j) - G of this lane's last step
+//   t0  = max(t, 0)
+//   hgL = v_add_u32_dpp(old = IOH, H, -G)   lanes 1..63: H(i,j-1) - G; lane 0 the inflow row
+//   H   = max3(hgL, hgO, t0)        hgO = H(i-1,j) - G of this lane's last step
 //   hgO = H - G
-// 6.75 VALU per step instead of 10.7; edges carry (H - G, H - G), which is also
+// 6.5 VALU per step instead of 10.7; edges carry (H - G, H - G), which is also
 // the exact (H - G_INIT, E - G_EXT) an affine consumer expects at G_INIT == G_EXT.
 template <int C, bool STREAM, bool RING, bool SLAB, bool LIN>
 __global__ void __launch_bounds__(256) sw_flow2_kernel(KParams kp) {
@@ -436,11 +446,16 @@ __global__ void __launch_bounds__(256) sw_flow2_kernel(KParams kp) {
                     }
                     auto step_lin = [&](auto b_c) __attribute__((always_inline)) {
                         constexpr int b = decltype(b_c)::value;
+                        // the dependency chain is H -> hgL (tied DPP-add straight out of H, the
+                        // wait states filled by hgO and t0) -> max3 -> H: the floor at 0 is
+                        // taken on t, off the chain (C2 4.21 -> 3.87 ms against the form
+                        // H = max(max3(hgL, hgO, 0), t) with hgL shifted out of hgO)
                         const int t = L0 + sbyte<b>(P[j >> 2]);
                         const int ioh = __builtin_amdgcn_update_dpp(L0, IOH, DPP_WAVE_SHL1, 0xF, 0xF, false);
-                        const int hgL = __builtin_amdgcn_update_dpp(IOH, hgO, DPP_WAVE_SHR1, 0xF, 0xF, false);
+                        int t0;
+                        const int hgL = dpp_add_shr1_tied_max0(IOH, H, neggo, hgO, t, t0);
                         IOH = ioh;
-                        H = max(vmax3(hgL, hgO, 0), t);
+                        H = vmax3(hgL, hgO, t0);
                         hgO = H - go;
                         M = max(M, t);
                         L0 = hgL;
