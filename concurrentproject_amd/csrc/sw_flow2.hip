@@ -65,14 +65,19 @@ __device__ __forceinline__ int dpp_add_shr1_tied(int old, int src, int k, int af
         : "+v"(old) : "v"(src), "v"(k), "v"(after));
     return old;
 }
-// The same with t0 = max(t, 0) computed inside, between the write of src and the
-// DPP read of it: `after` may then be the instruction right behind the one that
-// writes src, and the second wait state of the hazard is a useful instruction
-// (an s_nop there cost the C2 kernel 5 %).
-__device__ __forceinline__ int dpp_add_shr1_tied_max0(int old, int src, int k, int after, int t, int& t0) {
-    asm("v_max_i32_e32 %1, 0, %4\n\tv_add_u32_dpp %0, %2, %3 wave_shr:1 row_mask:0xf bank_mask:0xf ; dep %5"
-        : "+v"(old), "=&v"(t0) : "v"(src), "v"(k), "v"(t), "v"(after));
+// LIN: the I/O rotation ioh = wave_shl1(IOH) (lane 63 <- L0) and the tied DPP-add
+// of hgL in one asm: the rotation, which does not depend on H, is the second
+// instruction between the write of src (H) and its DPP read
+__device__ __forceinline__ int rot_dpp_add(int io, int& rot, int src, int k, int after) {
+    int old = io;
+    asm("v_mov_b32_dpp %1, %0 wave_shl:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_add_u32_dpp %0, %2, %3 wave_shr:1 row_mask:0xf bank_mask:0xf ; dep %4"
+        : "+v"(old), "+v"(rot) : "v"(src), "v"(k), "v"(after));
     return old;
+}
+// max(H - G, 0) for H >= 0 in one instruction (unsigned subtract, clamped at 0)
+__device__ __forceinline__ int sub_clamp0(int h, int g) {
+    return (int)__builtin_elementwise_sub_sat((unsigned)h, (unsigned)g);
 }
 
 // s_memrealtime with its wait inside the asm: nothing SMEM stays outstanding, so
@@ -115,11 +120,10 @@ constexpr int F2_CR = 256;
 // E(i,j-1) <= H(i,j-1) (H is a max over E), so max(E(i,j-1) - G, H(i,j-1) - G)
 // is the second term; the same for F.  The step keeps H only:
 //   t   = H(i-1,j-1) + s            (SDWA add, as above)
-//   t0  = max(t, 0)
 //   hgL = v_add_u32_dpp(old = IOH, H, -G)   lanes 1..63: H(i,j-1) - G; lane 0 the inflow row
-//   H   = max3(hgL, hgO, t0)        hgO = H(i-1,j) - G of this lane's last step
-//   hgO = H - G
-// 6.5 VALU per step instead of 10.7; edges carry (H - G, H - G), which is also
+//   H   = max3(hgL, hgO, t)         hgO = max(H(i-1,j) - G, 0) of this lane's last step
+//   hgO = max(H - G, 0)             v_sub_u32 with clamp (H >= 0): the floor at 0
+// 5.5 VALU per step instead of 10.7; edges carry (H - G, H - G), which is also
 // the exact (H - G_INIT, E - G_EXT) an affine consumer expects at G_INIT == G_EXT.
 template <int C, bool STREAM, bool RING, bool SLAB, bool LIN>
 __global__ void __launch_bounds__(256) sw_flow2_kernel(KParams kp) {
@@ -205,7 +209,8 @@ __global__ void __launch_bounds__(256) sw_flow2_kernel(KParams kp) {
         int nslow = 0;   // chunks whose inflow took the slow path (trace only)
         int fail_in = -1, fail_bp = -1;   // RING trace: chunk whose inflow / back-pressure wait timed out
         long long tl[5] = {0, 0, 0, 0, 0};   // SW_TIMELINE: wall clock at chunks 1, 2, 3, 50, 1000
-        int H = 0, E = 0, fh = -ge, hgO = -go, L0 = -go, ehP = -ge, M = 0;
+        // LIN keeps hgO clamped at 0 (see the step)
+        int H = 0, E = 0, fh = -ge, hgO = LIN ? 0 : -go, L0 = -go, ehP = -ge, M = 0;
         int IOH = -go, IOE = -ge;                 // rotating I/O registers (see the step)
         // -G_INIT, -G_EXT kept in VGPRs (operands of the DPP-adds, which take no SGPR)
         int neggo, negge;
@@ -446,17 +451,17 @@ __global__ void __launch_bounds__(256) sw_flow2_kernel(KParams kp) {
                     }
                     auto step_lin = [&](auto b_c) __attribute__((always_inline)) {
                         constexpr int b = decltype(b_c)::value;
-                        // the dependency chain is H -> hgL (tied DPP-add straight out of H, the
-                        // wait states filled by hgO and t0) -> max3 -> H: the floor at 0 is
-                        // taken on t, off the chain (C2 4.21 -> 3.87 ms against the form
-                        // H = max(max3(hgL, hgO, 0), t) with hgL shifted out of hgO)
+                        // 5.5 VALU: hgO = max(H - G, 0) in one clamped subtract carries the floor
+                        // at 0, so H = max(t, hgL, H_up - G, 0) = max3(hgL, hgO, t); hgL is a
+                        // tied DPP-add straight out of H, so the chain is H -> DPP-add -> max3
+                        // (C2 4.21 -> 3.64 ms, C5 285 -> 251 ms against H = max(max3(hgL, hgO, 0), t)
+                        // with hgO = H - G and hgL shifted out of hgO)
                         const int t = L0 + sbyte<b>(P[j >> 2]);
-                        const int ioh = __builtin_amdgcn_update_dpp(L0, IOH, DPP_WAVE_SHL1, 0xF, 0xF, false);
-                        int t0;
-                        const int hgL = dpp_add_shr1_tied_max0(IOH, H, neggo, hgO, t, t0);
+                        int ioh = L0;
+                        const int hgL = rot_dpp_add(IOH, ioh, H, neggo, hgO);
                         IOH = ioh;
-                        H = vmax3(hgL, hgO, t0);
-                        hgO = H - go;
+                        H = vmax3(hgL, hgO, t);
+                        hgO = sub_clamp0(H, go);
                         M = max(M, t);
                         L0 = hgL;
                     };
