@@ -141,9 +141,16 @@ def test_restatement_vs_reference_long_affine(oracle_mod):
 
 
 def test_config_c5_fixture(oracle_mod, golden):
-    """The C5 golden (N = 2^20, seed 1048576) belongs to the generator's pair and
-    names the engines that computed it (tests/golden/gen_c5.py)."""
+    """The C5 golden (N = 2^20, seed 1048576) belongs to the generator's pair and was
+    computed by two independent CPU engines that agree (tests/golden/gen_c5.py): the
+    reference's own LazySmith compiled from lazySmith.cpp:15-69 (1 thread, 3.8 h) and
+    the oracle's wavefront restatement; their result files are committed beside it."""
     c = golden("configs.json")["C5"]
     a, b = oracle_mod.gen_pair(c["seed"], c["N"])
     assert _sha(a, b) == c["sha256"]
-    assert c["score"] == 119470 and c["pinned_by"]
+    assert c["score"] == 119470
+    assert any("reference LazySmith" in s for s in c["pinned_by"]), c["pinned_by"]
+    assert any("swo_wavefront" in s for s in c["pinned_by"]), c["pinned_by"]
+    for eng in ("ref", "wavefront"):
+        r = golden("c5_%s.json" % eng)
+        assert r["score"] == c["score"] and r["sha256"] == c["sha256"], (eng, r)

@@ -96,6 +96,10 @@ def main():
     print(json.dumps(out))
     for k in list(range(0, 9)) + list(range(strips - 5, strips)):
         print(k, int(start[k]), int(first[k]), int(end[k]), int(spins[k]), round(run_ns[k] / steps, 2))
+    # pace along the pipeline: ns per step of each strip's run (first inflow -> end)
+    ks = list(range(0, strips, max(1, strips // 24)))
+    print("pace", [(k, round(run_ns[k] / steps, 1)) for k in ks])
+    print("end_lag_by_wave", [float(np.median(d_end[np.arange(d_end.size) % 4 == w])) for w in range(4)] if d_end.size else [])
 
 
 if __name__ == "__main__":

@@ -34,7 +34,10 @@ __global__ void tput(int* out, unsigned long long* cyc, int seed) {
     if constexpr (KIND == 10) asm volatile("v_pk_add_u16 %0, %0, %1 clamp" : "+v"(v##k) : "v"(a));             \
     if constexpr (KIND == 11) asm volatile("v_max_u16 %0, %0, %1" : "+v"(v##k) : "v"(a));                      \
     if constexpr (KIND == 12) asm volatile("v_sub_u32 %0, %0, %1 clamp" : "+v"(v##k) : "v"(a));                \
-    if constexpr (KIND == 13) asm volatile("v_max3_i16 %0, %0, %1, %2" : "+v"(v##k) : "v"(a), "v"(b));
+    if constexpr (KIND == 13) asm volatile("v_max3_i16 %0, %0, %1, %2" : "+v"(v##k) : "v"(a), "v"(b));           \
+    if constexpr (KIND == 14) asm volatile("v_pk_maximum3_f16 %0, %0, %1, %2" : "+v"(v##k) : "v"(a), "v"(b));   \
+    if constexpr (KIND == 15) asm volatile("v_add_u32_sdwa %0, %0, sext(%1) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1" : "+v"(v##k) : "v"(a)); \
+    if constexpr (KIND == 16) asm volatile("v_add_u32_dpp %0, %1, %2 wave_shr:1 row_mask:0xf bank_mask:0xf" : "+v"(v##k) : "v"(a), "v"(b));
         REP8(OP)
 #undef OP
     }
@@ -86,6 +89,9 @@ int main() {
         run<13>("v_max3_i16", t);
         run<7>("v_mov_dpp_wave_shr", t);
         run<8>("v_cndmask_vcc", t);
+        run<14>("v_pk_maximum3_f16", t);
+        run<15>("v_add_u32_sdwa", t);
+        run<16>("v_add_u32_dpp", t);
     }
     return 0;
 }
