@@ -53,6 +53,24 @@ constexpr int F2_R = 256;   // ring rows per link (power of two, >= 2C + 64)
 #ifndef SW_F2_HALFPUB
 #define SW_F2_HALFPUB 1     // workgroup-edge strips publish granules every half chunk
 #endif
+#ifndef SW_F2_HALFLDS
+#define SW_F2_HALFLDS 0     // 1: in-workgroup links hand off every half chunk (C2 3.63 -> 3.85 ms: slower)
+#endif
+#ifndef SW_F2_LOADER
+#define SW_F2_LOADER 1      // staged kernel: a fifth wave loads the workgroup's granule inflow into LDS
+#endif
+#ifndef SW_F2_LDQ
+#define SW_F2_LDQ 1         // loader: granule polls in flight (C2: 1 3.456, 2 3.473, 4 3.484 ms)
+#endif
+#ifndef SW_F2_LDSLEEP
+#define SW_F2_LDSLEEP 0     // loader: s_sleep units between polls of a round
+#endif
+#ifndef SW_F2_LDIDLE
+#define SW_F2_LDIDLE 0      // loader: s_sleep units after a round that moved nothing
+#endif
+#ifndef SW_F2_HALFIN_AHEAD
+#define SW_F2_HALFIN_AHEAD 4   // steps before mid-chunk at which the second half's inflow is read
+#endif
 
 // v_add_u32_dpp wave_shr:1 with the destination tied to 'old': lanes 1..63 get
 // src[l-1] + k, lane 0 (no source, bound_ctrl off) keeps old.  Inline asm because
@@ -125,20 +143,40 @@ constexpr int F2_CR = 256;
 //   hgO = max(H - G, 0)             v_sub_u32 with clamp (H >= 0): the floor at 0
 // 5.5 VALU per step instead of 10.7; edges carry (H - G, H - G), which is also
 // the exact (H - G_INIT, E - G_EXT) an affine consumer expects at G_INIT == G_EXT.
+// LOADER (the staged kernel): the workgroup's first strip does not poll HBM for
+// its inflow granules itself.  A fifth wave (no strip of its own) keeps
+// SW_F2_LDQ granule loads of the next 64 rows in flight, spaced SW_F2_LDSLEEP
+// apart, and moves every valid prefix into an LDS ring with a progress word, so
+// wave 0 takes its inflow like any in-workgroup link (half chunks, one LDS round
+// trip).  A published granule is then seen one load latency after it lands
+// instead of a sleep + reload round trip after wave 0 next looks.
+template <bool STREAM>
+constexpr bool f2_loader() { return SW_F2_LOADER && !STREAM; }
+template <bool STREAM>
+constexpr int f2_threads() { return f2_loader<STREAM>() ? 320 : 256; }
+
 template <int C, bool STREAM, bool RING, bool SLAB, bool LIN>
-__global__ void __launch_bounds__(256) sw_flow2_kernel(KParams kp) {
+__global__ void __launch_bounds__(f2_threads<STREAM>()) sw_flow2_kernel(KParams kp) {
     static_assert(!(RING || SLAB) || STREAM, "ring and slab kernels stream the row codes");
     static_assert(C % 4 == 0 && 64 % C == 0 && 2 * C + 64 <= F2_R, "chunk");
     // STREAM ring: during chunk c the reads span rows [k0 + C - 63, k0 + 2C) and the
     // writes rows [k0 + 2C, k0 + 3C): no slot is rewritten while still read
     static_assert(!STREAM || 3 * C + 63 <= F2_CR, "code ring");
+    static_assert(!SW_F2_HALFLDS || (SW_F2_SPEC == 0 && SW_F2_HALFIN_AHEAD % 4 == 0 && SW_F2_HALFIN_AHEAD <= C / 2),
+                  "half-chunk LDS links");
+    // rows per LDS hand-off: the consumer needs rows [k0, k0 + HL) at the start of a
+    // chunk and [k0 + HL, k0 + C) at its middle, so a link's lag is 64 + C/2 steps, not 64 + C
+    constexpr int HL = SW_F2_HALFLDS ? C / 2 : C;
     constexpr int R = F2_R;
+    constexpr bool LD = f2_loader<STREAM>();
+    constexpr int NT = f2_threads<STREAM>();
+    constexpr int NR = LD ? 5 : 4;           // LDS rings: one per compute wave (+ the loader's)
     constexpr int CRB = F2_CR + C + 64;      // STREAM ring + mirror + per-lane sinks, bytes per wave
     extern __shared__ unsigned char rc[];    // rc[row + 64]: 4..7 = A,C,G,T; 0 = no row (staged mode)
     __shared__ __attribute__((aligned(16))) unsigned char cring[STREAM ? 4 : 1][STREAM ? CRB : 16];
-    __shared__ int2 ring[4][R];              // ring w: outflow rows of wave w (row r in slot r mod R)
-    __shared__ int2 sink[4][64];             // lanes that publish nothing write here
-    __shared__ int prod[4], cons[4], psink[4][64];
+    __shared__ int2 ring[NR][R];             // ring w: outflow rows of wave w (row r in slot r mod R)
+    __shared__ int2 sink[NR][64];            // lanes that publish nothing write here
+    __shared__ int prod[NR], cons[NR], psink[NR][64];
     __shared__ int s_item;
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -156,13 +194,13 @@ __global__ void __launch_bounds__(256) sw_flow2_kernel(KParams kp) {
         const int m = pd.m;
         const int group = item - kp.item_base[pi];
         const int nloc = (m + 64 + C - 1) / C;   // lane 63's last row is out at step m + 63
-        if (tid < 4) { prod[tid] = 0; cons[tid] = 0; }
-        for (int i = tid; i < 4 * R; i += 256) ring[i / R][i % R] = make_int2(-go, -ge);
+        if (tid < NR) { prod[tid] = 0; cons[tid] = 0; }
+        for (int i = tid; i < NR * R; i += NT) ring[i / R][i % R] = make_int2(-go, -ge);
         const __amdgpu_buffer_rsrc_t row_rsrc =
             __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned char*>(kp.seq + pd.row_off), 0, m, RSRC_FLAGS);
         if constexpr (!STREAM) {
             const int nst = flow2_stage_bytes(m, C);
-            for (int i = tid * 4; i < nst; i += 1024) {
+            for (int i = tid * 4; i < nst; i += 4 * NT) {
                 unsigned w = 0;
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
@@ -175,6 +213,64 @@ __global__ void __launch_bounds__(256) sw_flow2_kernel(KParams kp) {
             }
         }
         __syncthreads();
+        if (LD && wave == 4) {   // the loader wave: granule inflow of strip 4 * group (not group 0)
+            if (group > 0 && 4 * group < pd.strips) {
+                const Edge le = group_edge(kp, pd, group - 1, (pd.strips + 3) / 4);
+                const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+                int2* const lring = ring[4];
+                int* const lprod = lane == 0 ? &prod[4] : &psink[4][lane];
+                int base = 0, sent = 0, cseen = 0;
+                bool lfail = false;
+                // rounds of SW_F2_LDQ polls of the current 64-row window, spaced SW_F2_LDSLEEP
+                // apart, then checked in issue order (no load crosses a round: a load whose
+                // destination is carried around the loop would be copied, and the copy waits for it)
+                while (base < m) {
+                    const int b0 = base, sent0 = sent;
+                    u32x4 q[SW_F2_LDQ];
+#pragma unroll
+                    for (int i = 0; i < SW_F2_LDQ; ++i) {
+                        q[i] = fetch_granules<64>(le, b0, lane, m);
+                        if (i + 1 < SW_F2_LDQ) __builtin_amdgcn_s_sleep(SW_F2_LDSLEEP);
+                    }
+#pragma unroll
+                    for (int i = 0; i < SW_F2_LDQ; ++i) {
+                        if (base == b0) {
+                            const int row = b0 + lane;
+                            const bool live = row < m;
+                            const bool ok = (!live) | granule_ok(q[i], le, row);
+                            const unsigned long long bal = __ballot(ok);
+                            const int lead = bal == ~0ull ? 64 : (int)__builtin_ctzll(~bal);
+                            if (b0 + lead > sent) {
+                                int2* const dst = ok && live ? &lring[row & (R - 1)] : &sink[4][lane];
+                                *dst = make_int2((int)q[i].y, (int)q[i].z);
+                                compiler_fence();
+                                sent = min(b0 + lead, m);
+                                *lprod = sent;   // after the ring writes (in-order DS)
+                            }
+                            if (lead == 64) base = b0 + 64;
+                        }
+                    }
+                    if (SW_F2_LDIDLE > 0 && sent == sent0) __builtin_amdgcn_s_sleep(SW_F2_LDIDLE);
+                    // the next window's slots: rows < base + 64 - R must be consumed by wave 0
+                    const int floor_rows = min(base, m) + 64 - R;
+                    while (cseen < floor_rows) {
+                        cseen = __builtin_amdgcn_readfirstlane(lds_load(&cons[0]));
+                        if (cseen >= floor_rows) break;
+                        __builtin_amdgcn_s_sleep(SW_SPIN_SLEEP);
+                        if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > kp.timeout_ticks) break;
+                    }
+                    if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > kp.timeout_ticks) {
+                        lfail = true;
+                        break;
+                    }
+                }
+                if (lfail && lane == 0) {
+                    atomicOr(&kp.ctrl->error, ERR_TIMEOUT);
+                    atomicMax(&kp.ctrl->err_item, (unsigned)(4 * group));
+                }
+            }
+            continue;
+        }
         const int strip = 4 * group + wave;
         if (strip >= pd.strips) continue;
         const int col = 63 * strip + lane;
@@ -182,7 +278,11 @@ __global__ void __launch_bounds__(256) sw_flow2_kernel(KParams kp) {
         // a multi-GPU column slab: the first strip takes the previous slab's edge, the
         // last one hands its lane-62 column (the next slab's left neighbour) on
         const int ngroups = (pd.strips + 3) / 4;
-        const int in_kind = wave > 0 ? FLOW_LDS : strip > 0 ? FLOW_GRANULE : kp.slab_in != nullptr ? FLOW_PEER : FLOW_NONE;
+        const int in_kind = wave > 0 || (LD && strip > 0) ? FLOW_LDS
+                            : strip > 0                   ? FLOW_GRANULE
+                            : kp.slab_in != nullptr       ? FLOW_PEER
+                                                          : FLOW_NONE;
+        const int in_w = wave > 0 ? wave - 1 : 4;   // the ring an LDS inflow comes from (4: the loader's)
         const int out_kind = strip + 1 >= pd.strips ? (kp.slab_out != nullptr ? FLOW_PEER : FLOW_NONE)
                              : wave < 3           ? FLOW_LDS
                                                   : FLOW_GRANULE;
@@ -220,7 +320,7 @@ __global__ void __launch_bounds__(256) sw_flow2_kernel(KParams kp) {
         // (no exec-mask branch, so the compiler counts LDS operations exactly)
         int* const prod_out = lane == 0 ? &prod[wave] : &psink[wave][lane];
         int* const cons_out = lane == 0 ? &cons[wave] : &psink[wave][lane];
-        int2* const in_ring = ring[wave > 0 ? wave - 1 : 0];
+        int2* const in_ring = ring[in_w < NR ? in_w : 0];
         int2* const out_ring = ring[wave];
         // per-lane code address: lane l reads rows k - l .. k - l + 3 (unaligned dword)
         const unsigned char* const code_base = rc + 64 - lane;
@@ -268,6 +368,8 @@ __global__ void __launch_bounds__(256) sw_flow2_kernel(KParams kp) {
 #pragma unroll
             for (int u = 0; u < C / 4; ++u) D[u] = load_u32_unaligned(code_at(0) + 4 * u);
             int cons_seen = 0;
+            int h_avail = 0;                     // SW_F2_HALFLDS: the mid-chunk inflow read
+            int2 h_v = make_int2(0, 0);
             int spec_avail = -1;                 // progress word read with spec_v (-1: none)
             int2 spec_v = make_int2(0, 0);
             // granule outflow at step k0 (chunk start, or mid-chunk with SW_F2_HALFPUB):
@@ -319,7 +421,7 @@ __global__ void __launch_bounds__(256) sw_flow2_kernel(KParams kp) {
                             }
                         }
                     }
-                    int2* const dst = lane >= 64 - C ? &out_ring[row_out & (R - 1)] : &sink[wave][lane];
+                    int2* const dst = lane >= 64 - HL ? &out_ring[row_out & (R - 1)] : &sink[wave][lane];
                     *dst = make_int2(IOH, LIN ? IOH : IOE);
                     compiler_fence();
                     *prod_out = max(0, k0 - 64);   // after the ring writes (in-order DS)
@@ -361,7 +463,7 @@ __global__ void __launch_bounds__(256) sw_flow2_kernel(KParams kp) {
                     newH = live ? (int)g.y : -go;
                     newE = live ? (int)g.z : -ge;
                 } else if constexpr (IN == FLOW_LDS) {
-                    const int need = min(k0 + C, m);
+                    const int need = min(k0 + HL, m);
                     int2 v;
                     if constexpr (SW_F2_SPEC > 0) {
                         // the rows were read speculatively during the last chunk, behind a read
@@ -369,10 +471,10 @@ __global__ void __launch_bounds__(256) sw_flow2_kernel(KParams kp) {
                         v = spec_v;
                         if (__builtin_amdgcn_readfirstlane(spec_avail) < need) {
                             ++nslow;
-                            int avail = __builtin_amdgcn_readfirstlane(lds_load(&prod[wave - 1]));
+                            int avail = __builtin_amdgcn_readfirstlane(lds_load(&prod[in_w]));
                             while (avail < need) {
                                 __builtin_amdgcn_s_sleep(SW_SPIN_SLEEP);
-                                avail = __builtin_amdgcn_readfirstlane(lds_load(&prod[wave - 1]));
+                                avail = __builtin_amdgcn_readfirstlane(lds_load(&prod[in_w]));
                                 if ((long long)__builtin_amdgcn_s_memrealtime() - t_start > kp.timeout_ticks) {
                                     failed = true;
                                     break;
@@ -385,16 +487,16 @@ __global__ void __launch_bounds__(256) sw_flow2_kernel(KParams kp) {
                         // the progress word and the chunk's rows in one LDS round trip (DS ops
                         // of a wave execute in order: rows read after a word that covers them
                         // are complete); re-read both until the word covers the chunk
-                        int avail = lds_load(&prod[wave - 1]);
+                        int avail = lds_load(&prod[in_w]);
                         compiler_fence();
-                        v = in_ring[(k0 + (lane & (C - 1))) & (R - 1)];
+                        v = in_ring[(k0 + (lane & (HL - 1))) & (R - 1)];
                         if (__builtin_amdgcn_readfirstlane(avail) < need) {
                             ++nslow;
                             do {
                                 __builtin_amdgcn_s_sleep(SW_SPIN_SLEEP);
-                                avail = lds_load(&prod[wave - 1]);
+                                avail = lds_load(&prod[in_w]);
                                 compiler_fence();
-                                v = in_ring[(k0 + (lane & (C - 1))) & (R - 1)];
+                                v = in_ring[(k0 + (lane & (HL - 1))) & (R - 1)];
                                 if ((long long)__builtin_amdgcn_s_memrealtime() - t_start > kp.timeout_ticks) {
                                     failed = true;
                                     break;
@@ -420,7 +522,7 @@ __global__ void __launch_bounds__(256) sw_flow2_kernel(KParams kp) {
                 IOE = newE;
                 if constexpr (IN == FLOW_LDS) {
                     compiler_fence();
-                    *cons_out = k0 + C;   // after the ring read (DS ops execute in order)
+                    *cons_out = k0 + HL;   // after the ring read (DS ops execute in order)
                 }
 #ifdef SW_TIMELINE
                 if (c == 0) t_first = realtime_waited();
@@ -441,9 +543,42 @@ __global__ void __launch_bounds__(256) sw_flow2_kernel(KParams kp) {
                         // lanes [64 - C/2, 64) hold this chunk's first C/2 outflow rows
                         if (j == C / 2) publish_granules_half(k0 + C / 2);
                     }
+                    if constexpr (OUT == FLOW_LDS && SW_F2_HALFLDS) {
+                        if (j == C / 2) publish(k0 + C / 2);
+                    }
+                    if constexpr (IN == FLOW_LDS && SW_F2_HALFLDS) {
+                        // the second half of the chunk's inflow: rows [k0 + C/2, k0 + C) go into
+                        // lanes [0, C/2) of the I/O registers just before step C/2, when lanes
+                        // [C/2, C) of the chunk start have rotated down there
+                        if (j == C / 2 - SW_F2_HALFIN_AHEAD) {
+                            h_avail = lds_load(&prod[in_w]);
+                            compiler_fence();
+                            h_v = in_ring[(k0 + HL + (lane & (HL - 1))) & (R - 1)];
+                        }
+                        if (j == C / 2) {
+                            const int need = min(k0 + C, m);
+                            if (__builtin_amdgcn_readfirstlane(h_avail) < need) {
+                                ++nslow;
+                                do {
+                                    __builtin_amdgcn_s_sleep(SW_SPIN_SLEEP);
+                                    h_avail = lds_load(&prod[in_w]);
+                                    compiler_fence();
+                                    h_v = in_ring[(k0 + HL + (lane & (HL - 1))) & (R - 1)];
+                                    if ((long long)__builtin_amdgcn_s_memrealtime() - t_start > kp.timeout_ticks) {
+                                        failed = true;
+                                        break;
+                                    }
+                                } while (__builtin_amdgcn_readfirstlane(h_avail) < need);
+                            }
+                            IOH = lane < HL ? h_v.x : IOH;
+                            if constexpr (!LIN) IOE = lane < HL ? h_v.y : IOE;
+                            compiler_fence();
+                            *cons_out = k0 + C;   // after the ring read
+                        }
+                    }
                     if constexpr (IN == FLOW_LDS && SW_F2_SPEC > 0) {
                         if (j == SW_F2_SPEC * C / 4) {   // speculative read of the next chunk's inflow
-                            spec_avail = lds_load(&prod[wave - 1]);
+                            spec_avail = lds_load(&prod[in_w]);
                             compiler_fence();
                             spec_v = in_ring[(k0 + C + (lane & (C - 1))) & (R - 1)];
                             compiler_fence();
@@ -526,7 +661,7 @@ hipError_t launch_c(const LaunchCfg& cfg, const KParams& kp, hipStream_t s) {
     // from a strip on the critical path); STREAM stages nothing, the rest is padding
     // STREAM: cfg.f2_wgs workgroups per CU (LDS just above 1/(wgs+1) of the CU's)
     const int wgs = STREAM ? std::max(1, std::min(cfg.f2_wgs, 4)) : 1;
-    const int pad = LDS_PER_CU / (wgs + 1) + 1024 - flow2_static_lds(C);
+    const int pad = LDS_PER_CU / (wgs + 1) + 1024 - flow2_static_lds(C, f2_loader<STREAM>() ? 5 : 4);
     const int dyn = STREAM ? pad : std::max(flow2_stage_bytes(cfg.max_m, C), pad);
     const int lim = flow2_stage_max(C) - (STREAM ? 4 * (F2_CR + C + 64) : 0);
     if (dyn > lim) return hipErrorInvalidValue;
@@ -534,8 +669,8 @@ hipError_t launch_c(const LaunchCfg& cfg, const KParams& kp, hipStream_t s) {
         const hipError_t e = raise_dyn_lds((const void*)sw_flow2_kernel<C, STREAM, RING, SLAB, LIN>, lim);
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL((sw_flow2_kernel<C, STREAM, RING, SLAB, LIN>), dim3(cfg.blocks), dim3(256), (size_t)dyn, s,
-                       kp);
+    hipLaunchKernelGGL((sw_flow2_kernel<C, STREAM, RING, SLAB, LIN>), dim3(cfg.blocks), dim3(f2_threads<STREAM>()),
+                       (size_t)dyn, s, kp);
     return hipGetLastError();
 }
 
@@ -552,7 +687,8 @@ hipError_t launch_v(const LaunchCfg& cfg, const KParams& kp, hipStream_t s) {
 template <int C>
 int waves_c() {
     int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)sw_flow2_kernel<C, false, false, false, false>, 256, 0) != hipSuccess)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)sw_flow2_kernel<C, false, false, false, false>,
+                                                     f2_threads<false>(), 0) != hipSuccess)
         return 4;
     return nb * 4;
 }

@@ -151,7 +151,8 @@ __host__ __device__ constexpr int flow2_strips(int n) { return n <= 64 ? 1 : (n 
 __host__ __device__ constexpr int flow2_stage_bytes(int m, int C) {
     return (64 + ((m + 64 + C - 1) / C + 1) * C + 8 + 15) & ~15;
 }
-__host__ __device__ constexpr int flow2_static_lds(int C) { return 4 * 256 * 8 + 4 * 64 * 8 + 4 * 64 * 4 + 64 + 0 * C; }
+// (rings: 4, or 5 with the staged kernel's loader wave, whose static LDS bounds the staged rows)
+__host__ __device__ constexpr int flow2_static_lds(int C, int rings = 5) { return rings * (256 * 8 + 64 * 8 + 64 * 4) + 64 + 0 * C; }
 __host__ __device__ constexpr int flow2_stage_max(int C) { return LDS_PER_CU - flow2_static_lds(C) - 256; }
 // sets the calling thread's sw_last_error() text (sw_engine.hip)
 void report_error(const char* msg);

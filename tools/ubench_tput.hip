@@ -37,7 +37,10 @@ __global__ void tput(int* out, unsigned long long* cyc, int seed) {
     if constexpr (KIND == 13) asm volatile("v_max3_i16 %0, %0, %1, %2" : "+v"(v##k) : "v"(a), "v"(b));           \
     if constexpr (KIND == 14) asm volatile("v_pk_maximum3_f16 %0, %0, %1, %2" : "+v"(v##k) : "v"(a), "v"(b));   \
     if constexpr (KIND == 15) asm volatile("v_add_u32_sdwa %0, %0, sext(%1) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1" : "+v"(v##k) : "v"(a)); \
-    if constexpr (KIND == 16) asm volatile("v_add_u32_dpp %0, %1, %2 wave_shr:1 row_mask:0xf bank_mask:0xf" : "+v"(v##k) : "v"(a), "v"(b));
+    if constexpr (KIND == 16) asm volatile("v_add_u32_dpp %0, %1, %2 wave_shr:1 row_mask:0xf bank_mask:0xf" : "+v"(v##k) : "v"(a), "v"(b)); \
+    if constexpr (KIND == 17) asm volatile("v_fma_f32 %0, %0, %1, %2" : "+v"(v##k) : "v"(a), "v"(b));            \
+    if constexpr (KIND == 18) asm volatile("v_add_f32 %0, %0, %1" : "+v"(v##k) : "v"(a));                       \
+    if constexpr (KIND == 19) asm volatile("v_add_u32 %0, %0, %1" : "+v"(v##k) : "v"(a));
         REP8(OP)
 #undef OP
     }
@@ -92,6 +95,9 @@ int main() {
         run<14>("v_pk_maximum3_f16", t);
         run<15>("v_add_u32_sdwa", t);
         run<16>("v_add_u32_dpp", t);
+        run<17>("v_fma_f32", t);
+        run<18>("v_add_f32", t);
+        run<19>("v_add_u32", t);
     }
     return 0;
 }
