@@ -113,6 +113,29 @@ __device__ __forceinline__ unsigned load_u32_unaligned(const unsigned char* p) {
     return v;
 }
 
+#ifndef SW_F2_WIDECODES
+#define SW_F2_WIDECODES 1   // a chunk's row codes in 16-B LDS reads (2 per 32 rows) instead of 4-B ones
+#endif
+// the C row codes lane l steps through in a chunk, C/4 dwords from p (any byte address)
+template <int C>
+__device__ __forceinline__ void load_codes(unsigned (&D)[C / 4], const unsigned char* p) {
+    if constexpr (SW_F2_WIDECODES) {
+        static_assert(C % 16 == 0, "16-B code reads");
+#pragma unroll
+        for (int u = 0; u < C / 4; u += 4) {
+            u32x4 v;
+            __builtin_memcpy(&v, p + 4 * u, 16);   // ds_read_b128 (unaligned LDS access)
+            D[u] = v.x;
+            D[u + 1] = v.y;
+            D[u + 2] = v.z;
+            D[u + 3] = v.w;
+        }
+    } else {
+#pragma unroll
+        for (int u = 0; u < C / 4; ++u) D[u] = load_u32_unaligned(p + 4 * u);
+    }
+}
+
 // signed byte b of w (SDWA src_sel:BYTE_b with sext)
 template <int B>
 __device__ __forceinline__ int sbyte(unsigned w) {
@@ -365,8 +388,7 @@ __global__ void __launch_bounds__(f2_threads<STREAM>()) sw_flow2_kernel(KParams 
             for (int i = 0; i < SW_F2_GPREF; ++i)
                 gq[i] = flow_granule(IN) ? fetch_granules<C, AIN>(in_e, i * C, lane, m) : u32x4{0u, 0u, 0u, 0u};
             unsigned D[C / 4];
-#pragma unroll
-            for (int u = 0; u < C / 4; ++u) D[u] = load_u32_unaligned(code_at(0) + 4 * u);
+            load_codes<C>(D, code_at(0));
             int cons_seen = 0;
             int h_avail = 0;                     // SW_F2_HALFLDS: the mid-chunk inflow read
             int2 h_v = make_int2(0, 0);
@@ -531,8 +553,7 @@ __global__ void __launch_bounds__(f2_threads<STREAM>()) sw_flow2_kernel(KParams 
                     put_codes(rq0, c + 2);
                     rq0 = raw_of(c + 3);
                 }
-#pragma unroll
-                for (int u = 0; u < C / 4; ++u) D[u] = load_u32_unaligned(code_at(k0 + C) + 4 * u);
+                load_codes<C>(D, code_at(k0 + C));
                 // ---- C anti-diagonal steps
 #pragma unroll
                 for (int j = 0; j < C; j += 4) {
