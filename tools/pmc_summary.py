@@ -75,6 +75,10 @@ def main():
         if not os.path.exists(stats):
             print("skip", cfg)
             continue
+        if os.path.getmtime(stats) < os.path.getmtime(LIB):
+            # the passes predate the library this would stamp them with (a failed or
+            # older gpurun call left them): never label old counters with a new build
+            sys.exit("%s is older than %s: re-run tools/prof_round.sh with this build" % (stats, LIB))
         shutil.copy(stats, os.path.join(prof, "%s_%s_kernel_stats.csv" % (rnd, cfg)))
         bench = os.path.join(src, "bench_%s.json" % cfg)
         if os.path.exists(bench):
