@@ -472,6 +472,15 @@ def main():
         }
         if extra is not None:
             out["batch_c3"] = extra
+        # the scaling series: N = 1 reports C2 as `value` (BASELINE configs[1]) with the C3 batch
+        # beside it; N > 1 reports C4 with the same 1024 pairs per GPU, so per-GPU efficiency
+        # compares value / n_gpus with the N = 1 line's batch_c3.value, not with its value
+        if workload == "batch" and world > 1:
+            out["scaling_note"] = ("C4: %d pairs N=%d per GPU; per-GPU baseline = the N=1 line's batch_c3.value "
+                                   "(C3, the same per-GPU work)" % (P, N))
+        elif workload == "pair" and world == 1 and extra is not None:
+            out["scaling_note"] = ("N>1 lines report C4 (1024 pairs N=8192 per GPU); their per-GPU baseline is "
+                                   "batch_c3.value here, not value (C2)")
         if workload != "batch" and affine is not None:
             out["affine_step"] = affine
         if world == 1 and not args.no_cpu_baseline:
