@@ -240,6 +240,33 @@ def test_flow2_ragged(engine, oracle_mod):
         engine.set_option("orient", 0)
 
 
+def test_flow2_loader_wave(engine, oracle_mod):
+    """The staged flow2 kernel's loader wave (a fifth wave that moves a workgroup's
+    inflow granules into LDS for wave 0): pairs of many 4-strip groups on grids of
+    1, 2, 3 and 7 workgroups (a group's producer ran on another or the same
+    workgroup, or finished long before), row counts around the loader's 64-row
+    window, several pairs per launch, linear-gap and affine steps."""
+    rng = np.random.default_rng(2024)
+    shapes = [(1100, 63), (1100, 64), (1100, 65), (2000, 127), (2000, 129), (3000, 1000), (4096, 2049)]
+    pairs = [(_rand_dna(rng, n), _rand_dna(rng, m)) for n, m in shapes]
+    engine.set_option("orient", 1)
+    engine.set_option("mode", 5)
+    try:
+        for prm in (engine.Params(), engine.Params(2, -3, 5, 2)):
+            op = oracle_mod.Params(prm.match, prm.mismatch, prm.gap_init, prm.gap_ext)
+            exp = [oracle_mod.score_linear(a, b, op) for a, b in pairs]
+            for blocks in (1, 2, 3, 7, 0):
+                engine.set_option("blocks", blocks)
+                assert engine.score_batch(pairs, prm) == exp, (prm, blocks)
+                st = engine.last_stats()
+                assert st["mode"] == 5 and not st["variant"] & 2, st   # the staged kernel
+            assert [engine.score(a, b, prm) for a, b in pairs] == exp, prm
+    finally:
+        engine.set_option("mode", -1)
+        engine.set_option("blocks", 0)
+        engine.set_option("orient", 0)
+
+
 def test_flow2_streamed_rows(engine, oracle_mod):
     """flow2 with the row codes streamed through per-wave LDS rings (rows too long
     to stage, the C5 path): forced on the ragged flow2 shapes and chosen
