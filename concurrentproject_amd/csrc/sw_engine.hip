@@ -378,6 +378,9 @@ int finalize_mode(Job& job, const Params& prm) {
         if (flow2_fits(job, prm)) {
             plan_flow2(job);
             job.f2_stream = job.ring || !flow2_staged(job, max_m);   // ring mode runs with streamed codes
+            // ring mode (one pair of many groups per CU, C5): throughput-bound, so 64-row chunks
+            // (half the per-chunk work per step) beat the shorter hand-off lag of 32 (C5 249 -> 220 ms)
+            if (job.ring && g_opt_C.load() == 0) job.C = 64;
             return 0;
         }
         if (job.mode == MODE_FLOW2) {
@@ -560,7 +563,7 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
     cfg.f2_stream = f2s;
     cfg.f2_wgs = f2_wgs;
     // G_INIT == G_EXT: the exact linear-gap step (sw_flow2.hip LIN), unless disabled
-    cfg.f2_lin = ((job.mode == MODE_FLOW2 && job.C == 32) || (job.mode == MODE_DUO && cfg.duo_f16)) &&
+    cfg.f2_lin = ((job.mode == MODE_FLOW2 && (job.C == 32 || job.C == 64)) || (job.mode == MODE_DUO && cfg.duo_f16)) &&
                  prm.gap_init == prm.gap_ext && g_opt_linear.load() != 0;
     const int wpc = waves_per_cu(c, cfg);
     const int items = job.item_base[np];

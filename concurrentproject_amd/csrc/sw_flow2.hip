@@ -720,10 +720,11 @@ bool flow2_variant_exists(int C) { return C == 16 || C == 32 || C == 64; }
 
 hipError_t launch_sw_flow2(const LaunchCfg& cfg, const KParams& kp, hipStream_t stream) {
     switch (cfg.C) {
-        // the linear-gap step (G_INIT == G_EXT) is built for the default chunk only
+        // the linear-gap step (G_INIT == G_EXT) is built for 32-row (latency-bound pairs) and
+        // 64-row chunks (ring mode, throughput-bound)
         case 16: return launch_v<16, false>(cfg, kp, stream);
         case 32: return cfg.f2_lin ? launch_v<32, true>(cfg, kp, stream) : launch_v<32, false>(cfg, kp, stream);
-        case 64: return launch_v<64, false>(cfg, kp, stream);
+        case 64: return cfg.f2_lin ? launch_v<64, true>(cfg, kp, stream) : launch_v<64, false>(cfg, kp, stream);
         default: return hipErrorInvalidValue;
     }
 }

@@ -209,14 +209,14 @@ def test_flow2_ragged(engine, oracle_mod):
             engine.set_option("mode", 5)
             for C in (16, 32, 64):
                 engine.set_option("C", C)
-                # G_INIT == G_EXT at C = 32: the linear-gap step (auto) and the affine step (linear = 0)
-                for lin in ((-1, 0) if prm.gap_init == prm.gap_ext and C == 32 else (-1,)):
+                # G_INIT == G_EXT at C = 32 / 64: the linear-gap step (auto) and the affine step (linear = 0)
+                for lin in ((-1, 0) if prm.gap_init == prm.gap_ext and C in (32, 64) else (-1,)):
                     engine.set_option("linear", lin)
                     got = [engine.score(a, b, prm) for a, b in pairs]
                     assert got == exp, (C, prm, lin)
                     st = engine.last_stats()
                     assert st["mode"] == 5
-                    assert bool(st["variant"] & 8) == (lin == -1 and prm.gap_init == prm.gap_ext and C == 32), st
+                    assert bool(st["variant"] & 8) == (lin == -1 and prm.gap_init == prm.gap_ext and C in (32, 64)), st
                     assert engine.score_batch(pairs, prm) == exp, (C, prm, lin)
                 engine.set_option("linear", -1)
             engine.set_option("C", 0)
