@@ -3,20 +3,29 @@
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--workload auto|pair|batch|slab]
 
+Ranks: one process per GPU.  Under torchrun (RANK/WORLD_SIZE set) this process
+is one rank; standalone with --gpus N > 1 it checks that N GPUs are visible
+(exit 2 otherwise), starts N ranks of itself (concurrentproject_amd.launch:
+rank r on device r, MASTER_ADDR 127.0.0.1) and exits with their status.  The
+ranks form an "nccl" (RCCL) group; `n_gpus` is its world size.
+
 Workloads (BASELINE.json configs; synthetic uniform {A,C,G,T}, generator of
 cudaSmithM.cu:200-212, sequences resident in HBM before the timed region):
-  pair   C2: one pair N=65536 (seed 65536), one launch per step.  With --gpus N
-         the global batch is N such pairs (seeds 65536+k), one per rank, the
-         per-pair scores gathered to rank 0 over RCCL every step.
+  pair   C2: one pair N=65536 (seed 65536), one launch per step.  With N ranks
+         the global batch is N such pairs (seeds 65536+rank), one per rank, the
+         per-pair scores gathered to rank 0 over RCCL every step (weak scaling
+         of the same per-GPU work as the N=1 line).
   batch  C3/C4: 1024 pairs of N=8192 per GPU; rank r scores pairs
          [1024r, 1024r+1024) (seeds 8192+k), then the per-pair int32 scores are
-         gathered to rank 0 with RCCL (torch.distributed "nccl") every step.
-         --gpus 8 is config C4 (8192 pairs).
-  slab   C5: one pair N=2^20 (seed 1048576); with --gpus N its columns are cut
-         into one slab per rank (dist.ColumnSlabs).
-  auto   N=1: C2 (configs[1], the metric's single-GPU config), and the C3 batch
-         measured after it as the extra key "batch_c3".  N>1: the C4 batch
-         (configs[3]: the >= 7.5x target of north_star is stated on batched pairs).
+         gathered to rank 0 with RCCL every step.  8 ranks = config C4.
+  slab   C5: one pair N=2^20 (seed 1048576); with N ranks its columns are cut
+         into one slab per rank (dist.ColumnSlabs); per-rank kernel times and
+         the pipeline fill are reported beside `value`.
+  auto   `value` is the pair workload at every N (C2 at N=1: configs[1], the
+         metric's single-GPU config), so the 1/2/4/8 series compares the same
+         per-GPU work.  The batched config is measured after it on the same
+         ranks and reported as "batch_c3" (N=1) or "batch_c4" (N>1: 1024 pairs
+         per GPU, C4 at N=8; north_star's >= 7.5x is stated on batched pairs).
 A step is one full pass of the hot path over the step's input; `value` is the
 whole-job GCUPS (sum of n*m over all ranks' pairs / max-over-ranks time).
 
@@ -52,7 +61,8 @@ VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12   # T lane-ops/s = 78.64
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one per GPU); standalone N > 1 spawns them, under torchrun it must equal WORLD_SIZE")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--workload", default="auto", choices=["auto", "pair", "batch", "slab"])
@@ -267,17 +277,42 @@ def run_batch(sw, torch, dist, world, rank, N, P, steps, warmup):
     return t_max, kern_ms, allsc, npairs * N * N, sw.last_stats()
 
 
+def start_ranks(args) -> int | None:
+    """Standalone `--gpus N` (N > 1, no launcher variables): check the devices and run
+    N ranks of this script (concurrentproject_amd.launch.spawn_ranks); returns the
+    job's exit status.  None when this process is to run as a rank itself.  Nothing
+    here initialises the GPU (device_count only), and the ranks are child processes."""
+    from concurrentproject_amd.launch import LaunchError, launcher_env, require_devices, spawn_ranks
+    if launcher_env() or (args.gpus or 1) <= 1:
+        return None
+    try:
+        require_devices(args.gpus)
+    except LaunchError as e:
+        print("bench.py: %s" % e, file=sys.stderr, flush=True)
+        return 2
+    return spawn_ranks(args.gpus, [sys.executable, os.path.abspath(__file__)] + sys.argv[1:])
+
+
 def main():
     args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    status = start_ranks(args)
+    if status is not None:
+        sys.exit(status)
+    from concurrentproject_amd.launch import launcher_env, rank_env, visible_devices
+    world, rank, local = rank_env()
+    if args.gpus is not None and args.gpus != world:
+        sys.exit("bench.py: --gpus %d but the launcher started %d ranks (WORLD_SIZE)" % (args.gpus, world))
+    if local >= visible_devices():
+        sys.exit("bench.py: rank %d needs GPU %d, this host shows %d" % (rank, local, visible_devices()))
     import torch
     torch.cuda.set_device(local)
     dist = None
-    if world > 1 or "TORCHELASTIC_RUN_ID" in os.environ:   # launched by torch.distributed.run
+    rccl = None
+    if world > 1 or launcher_env():
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        world, rank = dist.get_world_size(), dist.get_rank()
+        rccl = {"backend": dist.get_backend(), "world_size": world}
     import concurrentproject_amd as sw
     params = tuple(int(x) for x in args.params.split(","))
     sw.set_params(sw.Params(*params))
@@ -295,7 +330,8 @@ def main():
 
     workload = args.workload
     if workload == "auto":
-        workload = "pair" if world == 1 else "batch"
+        workload = "pair"     # the same per-GPU work at every N (module docstring)
+    slab_ranks = None
 
     extra = None
     step_ns = None
@@ -387,6 +423,17 @@ def main():
         st = sw.last_stats()
         first = gathered[0][0].item() if gathered[0] is not None else scores[0].item()
         if slabs is not None:
+            # every rank's launch-to-end kernel time: rank r's includes the wait for
+            # rank r-1's edge, so the spread over ranks is the pipeline fill
+            kt = torch.tensor([avg_kern_ms], dtype=torch.float64, device="cuda")
+            allk = [torch.zeros_like(kt) for _ in range(world)]
+            dist.all_gather(allk, kt)
+            per_rank = [round(float(x.item()), 4) for x in allk]
+            slab_ranks = {"per_rank_kernel_ms": per_rank,
+                          "per_rank_columns": [slabs.bounds[r + 1] - slabs.bounds[r] for r in range(world)],
+                          "pipeline_fill_ms": round(per_rank[-1] - per_rank[0], 4),
+                          "note": "rank 0 runs at its own pace; rank r's kernel also waits for the first "
+                                  "edge rows of rank r-1, so last - first is the fill of the R-1 hops"}
             slabs.close()
         if slab_buf is not None:
             slab_buf.free()
@@ -421,18 +468,24 @@ def main():
                           "parity": ok, "note": "option linear=0: the general affine (E, F) step on the C2 pair"}
             finally:
                 sw.set_option("linear", -1)
-        # N=1: the batched config (C3) measured right after, as an extra key
-        if workload == "pair" and world == 1 and args.workload == "auto" and not args.no_extra:
-            bt, bk, bsc, bcells, bst = run_batch(sw, torch, None, 1, 0, 8192, 1024, max(3, args.steps // 2), 1)
+        # the batched config measured right after on the same ranks, as an extra key:
+        # C3 at N=1, 1024 pairs per GPU sharded + RCCL-gathered at N>1 (C4 at N=8)
+        if workload == "pair" and args.workload == "auto" and not args.no_extra:
+            bsteps = max(3, args.steps // 2)
+            bt, bk, bsc, bcells, bst = run_batch(sw, torch, dist, world, rank, 8192, 1024, bsteps, 1)
             ref = gold.get("C4", gold.get("C3", {})).get("scores", [])
-            extra = {"workload": "C3 batch of 1024 pairs N=8192 (seeds 8192+k)", "value": round(bcells * max(3, args.steps // 2) / bt / 1e9, 3),
-                     "unit": "GCUPS", "kernel_ms_per_launch": round(bk, 4),
+            extra = {"workload": ("C3 batch of 1024 pairs N=8192 (seeds 8192+k)" if world == 1 else
+                                  "C4-order batch: %d pairs N=8192, 1024 per GPU (seeds 8192+k), RCCL gather"
+                                  % (1024 * world)),
+                     "n_gpus": world, "value": round(bcells * world * bsteps / bt / 1e9, 3),
+                     "unit": "GCUPS", "ms_per_step": round(bt / bsteps * 1e3, 4), "kernel_ms_per_launch": round(bk, 4),
                      "kernel_gcups": round(bcells / (bk * 1e-3) / 1e9, 3),
-                     "parity": ("ok" if bsc == ref[:len(bsc)] else "MISMATCH") if defaults and len(ref) >= 1024
-                     else "unchecked",
+                     "parity": ("ok" if bsc == ref[:len(bsc)] else "MISMATCH")
+                     if defaults and len(ref) >= len(bsc) == 1024 * world else "unchecked",
                      "kernel": {3: "duo", 1: "pairwg"}.get(bst["mode"], bst["mode"]),
                      "dtype": "u16x2 (packed, exact: scores < 2^16)" if bst["mode"] == 3 else "int32",
                      "roofline": roofline("batch", bcells, bk)}
+        if extra is not None and world == 1:
             # the same batch on the int32 pair-per-workgroup kernel (no 16-bit packing)
             sw.set_option("mode", 1)
             try:
@@ -470,17 +523,19 @@ def main():
             "roofline": roofline(workload if args.slab_of <= 1 else "slab_part", per_launch_cells, avg_kern_ms,
                                  step_ns, cfg["N"], cfg["N"]),
         }
+        if rccl is not None:
+            out["rccl_world"] = rccl
         if extra is not None:
-            out["batch_c3"] = extra
-        # the scaling series: N = 1 reports C2 as `value` (BASELINE configs[1]) with the C3 batch
-        # beside it; N > 1 reports C4 with the same 1024 pairs per GPU, so per-GPU efficiency
-        # compares value / n_gpus with the N = 1 line's batch_c3.value, not with its value
-        if workload == "batch" and world > 1:
-            out["scaling_note"] = ("C4: %d pairs N=%d per GPU; per-GPU baseline = the N=1 line's batch_c3.value "
-                                   "(C3, the same per-GPU work)" % (P, N))
-        elif workload == "pair" and world == 1 and extra is not None:
-            out["scaling_note"] = ("N>1 lines report C4 (1024 pairs N=8192 per GPU); their per-GPU baseline is "
-                                   "batch_c3.value here, not value (C2)")
+            out["batch_c3" if world == 1 else "batch_c4"] = extra
+        if slab_ranks is not None:
+            out["slab_ranks"] = slab_ranks
+        # the scaling series: `value` is the same per-GPU work at every N (one C2-size pair per
+        # GPU), so value(N) / (N * value(1)) is the efficiency; the batched series is
+        # batch_c4.value(N) against the N = 1 line's batch_c3.value (1024 pairs per GPU in both)
+        if workload == "pair" and args.workload == "auto":
+            out["scaling_note"] = ("value: one C2-size pair (N=%d) per GPU at every N; batched pairs: %s.value "
+                                   "vs the N=1 line's batch_c3.value (1024 pairs N=8192 per GPU)"
+                                   % (N, "batch_c3" if world == 1 else "batch_c4"))
         if workload != "batch" and affine is not None:
             out["affine_step"] = affine
         if world == 1 and not args.no_cpu_baseline:

@@ -66,13 +66,14 @@ def build(verbose: bool = False) -> str:
 
 
 def source_stamp() -> str:
-    """sha256 over the engine's sources and build flags (csrc/*.hip, *.h, Makefile and
+    """sha256 over the engine's sources and build flags (csrc/*.hip, *.h, *.cpp, Makefile and
     include/algoGPU.h): identifies the kernels a profile was taken with, across rebuilds."""
     import glob
     import hashlib
     h = hashlib.sha256()
     csrc = os.path.join(HERE, "csrc")
     files = sorted(glob.glob(os.path.join(csrc, "*.hip")) + glob.glob(os.path.join(csrc, "*.h")) +
+                   glob.glob(os.path.join(csrc, "*.cpp")) +
                    [os.path.join(csrc, "Makefile"), os.path.join(HERE, "..", "include", "algoGPU.h")])
     for f in files:
         h.update(os.path.basename(f).encode())

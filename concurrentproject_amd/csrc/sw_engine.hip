@@ -527,13 +527,40 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
         const int per_cu = job.item_base[np] / c->cus;
         f2_wgs = o > 0 ? (int)o : job.ring ? std::min(F2_WGS_MAX, std::max(1, per_cu / 2)) : per_cu >= 4 ? 2 : 1;
     }
+    // G_INIT == G_EXT: the exact linear-gap step (sw_flow2.hip LIN), unless disabled
+    const bool f2_lin = ((job.mode == MODE_FLOW2 && (job.C == 32 || job.C == 64)) ||
+                         (job.mode == MODE_DUO && job.duo_f16)) &&
+                        prm.gap_init == prm.gap_ext && g_opt_linear.load() != 0;
+    // read once: it sizes the ring arena here and addresses it in the kernel (kp.ring_rows)
+    const long long ring_rows = g_opt_ring_rows.load();
     int ring_blocks = 0, wrap_rows = 0;
     if (job.ring) {
+        // the static deal needs every block resident at once: ask the runtime how many
+        // workgroups of the instantiation this launch runs fit a CU (registers, waves and
+        // the LDS pad of f2_wgs), and take no more per CU than that
+        LaunchCfg probe{1, job.C, true, 0, MODE_FLOW2, 0};
+        probe.f2_stream = true;
+        probe.f2_lin = f2_lin;
+        int fit = 0;
+        for (;; --f2_wgs) {
+            probe.f2_wgs = f2_wgs;
+            fit = flow2_stream_resident(probe, true, edge != nullptr);
+            if (fit >= f2_wgs || f2_wgs == 1) break;
+        }
+        if (fit < 1) {
+            set_err("flow2 ring mode: the runtime reports %d resident workgroups per CU for its kernel", fit);
+            return -1;
+        }
         ring_blocks = std::min(job.item_base[np], c->cus * f2_wgs);
         if (g_opt_blocks.load() > 0) ring_blocks = (int)std::min<long long>(g_opt_blocks.load(), job.item_base[np]);
+        if (ring_blocks > c->cus * fit) {
+            set_err("flow2 ring mode needs all %d workgroups co-resident (%d fit per CU, %d CUs)", ring_blocks, fit,
+                    c->cus);
+            return -1;
+        }
         wrap_rows = 1;
         while (wrap_rows < job.pairs[0].m) wrap_rows *= 2;
-        job.bnd_granules = (uint64_t)(ring_blocks - 1) * (uint64_t)g_opt_ring_rows.load() + (uint64_t)wrap_rows;
+        job.bnd_granules = (uint64_t)(ring_blocks - 1) * (uint64_t)ring_rows + (uint64_t)wrap_rows;
         if (c->cons.ensure((size_t)ring_blocks * RING_CONS_STRIDE, s)) return -1;
         HIPCHK(hipMemsetAsync(c->cons.p, 0, (size_t)ring_blocks * RING_CONS_STRIDE * sizeof(unsigned), s));
     }
@@ -562,9 +589,7 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
     // flow2 ring and slab kernels always stream the row codes (sw_flow2.hip launch_v)
     cfg.f2_stream = f2s;
     cfg.f2_wgs = f2_wgs;
-    // G_INIT == G_EXT: the exact linear-gap step (sw_flow2.hip LIN), unless disabled
-    cfg.f2_lin = ((job.mode == MODE_FLOW2 && (job.C == 32 || job.C == 64)) || (job.mode == MODE_DUO && cfg.duo_f16)) &&
-                 prm.gap_init == prm.gap_ext && g_opt_linear.load() != 0;
+    cfg.f2_lin = f2_lin;
     const int wpc = waves_per_cu(c, cfg);
     const int items = job.item_base[np];
     long long blocks = g_opt_blocks.load();
@@ -579,16 +604,7 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
         // the CU count would only park extra workgroups until a CU frees up
         if (job.mode == MODE_FLOW2) blocks = std::min<long long>(blocks, (long long)c->cus * f2_wgs);
     }
-    if (job.ring) {
-        // the static item deal needs every block resident at once; flow2 pads its LDS to
-        // more than half a CU's, so one workgroup per CU
-        if (ring_blocks > c->cus * f2_wgs) {
-            set_err("flow2 ring mode needs all %d workgroups co-resident (%d per CU, %d CUs)", ring_blocks, f2_wgs,
-                    c->cus);
-            return -1;
-        }
-        blocks = ring_blocks;
-    }
+    if (job.ring) blocks = ring_blocks;   // checked co-resident above
     cfg.blocks = (int)std::max<long long>(1, blocks);
 
     KParams kp{};
@@ -621,7 +637,7 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
     kp.timeout_ticks = g_opt_timeout.load() * 100000000LL;   // s_memrealtime: 100 MHz
     kp.trace = reinterpret_cast<unsigned long long*>(g_opt_trace.load());
     if (job.ring) {
-        kp.ring_rows = (int)g_opt_ring_rows.load();
+        kp.ring_rows = (int)ring_rows;
         kp.wrap_rows = wrap_rows;
         kp.ring_cons = c->cons.p;
     }

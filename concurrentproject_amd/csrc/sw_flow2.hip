@@ -675,24 +675,55 @@ __global__ void __launch_bounds__(f2_threads<STREAM>()) sw_flow2_kernel(KParams 
     }
 }
 
+// Dynamic LDS of a launch (*lim: the most it may be).  At least half the CU's LDS
+// for the staged kernel: one workgroup per CU, so no strip ever shares a SIMD with
+// another (a co-resident waiting workgroup's polls steal issue slots from a strip
+// on the critical path); STREAM stages nothing, the rest is padding that admits
+// cfg.f2_wgs workgroups per CU (LDS just above 1/(wgs+1) of the CU's).
+template <int C, bool STREAM>
+int flow2_dyn_lds(const LaunchCfg& cfg, int* lim) {
+    const int wgs = STREAM ? std::max(1, std::min(cfg.f2_wgs, F2_WGS_MAX)) : 1;
+    const int pad = LDS_PER_CU / (wgs + 1) + 1024 - flow2_static_lds(C, f2_loader<STREAM>() ? 5 : 4);
+    *lim = flow2_stage_max(C) - (STREAM ? 4 * (F2_CR + C + 64) : 0);
+    return STREAM ? pad : std::max(flow2_stage_bytes(cfg.max_m, C), pad);
+}
+
+template <int C, bool STREAM, bool RING = false, bool SLAB = false, bool LIN = false>
+hipError_t prepare_c(const LaunchCfg& cfg, int* dyn) {
+    int lim = 0;
+    *dyn = flow2_dyn_lds<C, STREAM>(cfg, &lim);
+    if (*dyn > lim) return hipErrorInvalidValue;
+    if (*dyn > 64 * 1024)   // raise the dynamic-LDS limit (once per variant and device)
+        return raise_dyn_lds((const void*)sw_flow2_kernel<C, STREAM, RING, SLAB, LIN>, lim);
+    return hipSuccess;
+}
+
 template <int C, bool STREAM, bool RING = false, bool SLAB = false, bool LIN = false>
 hipError_t launch_c(const LaunchCfg& cfg, const KParams& kp, hipStream_t s) {
-    // at least half the CU's LDS: one workgroup per CU, so no strip ever shares a
-    // SIMD with another (a co-resident waiting workgroup's polls steal issue slots
-    // from a strip on the critical path); STREAM stages nothing, the rest is padding
-    // STREAM: cfg.f2_wgs workgroups per CU (LDS just above 1/(wgs+1) of the CU's)
-    const int wgs = STREAM ? std::max(1, std::min(cfg.f2_wgs, 4)) : 1;
-    const int pad = LDS_PER_CU / (wgs + 1) + 1024 - flow2_static_lds(C, f2_loader<STREAM>() ? 5 : 4);
-    const int dyn = STREAM ? pad : std::max(flow2_stage_bytes(cfg.max_m, C), pad);
-    const int lim = flow2_stage_max(C) - (STREAM ? 4 * (F2_CR + C + 64) : 0);
-    if (dyn > lim) return hipErrorInvalidValue;
-    if (dyn > 64 * 1024) {   // raise the dynamic-LDS limit (once per variant and device)
-        const hipError_t e = raise_dyn_lds((const void*)sw_flow2_kernel<C, STREAM, RING, SLAB, LIN>, lim);
-        if (e != hipSuccess) return e;
-    }
+    int dyn = 0;
+    const hipError_t e = prepare_c<C, STREAM, RING, SLAB, LIN>(cfg, &dyn);
+    if (e != hipSuccess) return e;
     hipLaunchKernelGGL((sw_flow2_kernel<C, STREAM, RING, SLAB, LIN>), dim3(cfg.blocks), dim3(f2_threads<STREAM>()),
                        (size_t)dyn, s, kp);
     return hipGetLastError();
+}
+
+// Workgroups per CU the runtime will keep resident for the streamed instantiation a
+// launch of cfg would run (its registers, waves and the LDS of cfg.f2_wgs): what
+// ring mode's static deal must not exceed (every block resident).  -1 on error.
+template <int C, bool RING, bool SLAB, bool LIN>
+int resident_c(const LaunchCfg& cfg) {
+    int dyn = 0, nb = 0;
+    if (prepare_c<C, true, RING, SLAB, LIN>(cfg, &dyn) != hipSuccess) return -1;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)sw_flow2_kernel<C, true, RING, SLAB, LIN>,
+                                                     f2_threads<true>(), (size_t)dyn) != hipSuccess)
+        return -1;
+    return nb;
+}
+template <int C, bool LIN>
+int resident_v(const LaunchCfg& cfg, bool ring, bool slab) {
+    if (slab) return ring ? resident_c<C, true, true, LIN>(cfg) : resident_c<C, false, true, LIN>(cfg);
+    return ring ? resident_c<C, true, false, LIN>(cfg) : resident_c<C, false, false, LIN>(cfg);
 }
 
 // the instantiation a launch needs: ring edges, slab edges, streamed or staged codes
@@ -726,6 +757,15 @@ hipError_t launch_sw_flow2(const LaunchCfg& cfg, const KParams& kp, hipStream_t 
         case 32: return cfg.f2_lin ? launch_v<32, true>(cfg, kp, stream) : launch_v<32, false>(cfg, kp, stream);
         case 64: return cfg.f2_lin ? launch_v<64, true>(cfg, kp, stream) : launch_v<64, false>(cfg, kp, stream);
         default: return hipErrorInvalidValue;
+    }
+}
+
+int flow2_stream_resident(const LaunchCfg& cfg, bool ring, bool slab) {
+    switch (cfg.C) {
+        case 16: return resident_v<16, false>(cfg, ring, slab);
+        case 32: return cfg.f2_lin ? resident_v<32, true>(cfg, ring, slab) : resident_v<32, false>(cfg, ring, slab);
+        case 64: return cfg.f2_lin ? resident_v<64, true>(cfg, ring, slab) : resident_v<64, false>(cfg, ring, slab);
+        default: return -1;
     }
 }
 

@@ -126,7 +126,7 @@ struct LaunchCfg {
     bool duo_f16 = false;   // MODE_DUO: max3 through v_pk_maximum3_f16 (every value < 0x7C00)
     bool f2_stream = false; // MODE_FLOW2: row codes streamed through per-wave LDS rings (rows too long to stage)
     int f2_wgs = 1;         // MODE_FLOW2 streamed: workgroups per CU (LDS pad sized to admit exactly this many)
-    bool f2_lin = false;    // G_INIT == G_EXT, the exact linear-gap step: MODE_FLOW2 at C = 32 (sw_flow2.hip
+    bool f2_lin = false;    // G_INIT == G_EXT, the exact linear-gap step: MODE_FLOW2 at C = 32 or 64 (sw_flow2.hip
                             // LIN) and MODE_DUO with duo_f16 (sw_kernels.hip StripDuo LIN)
 };
 constexpr int F2_WGS_MAX = 4;   // flow2 streamed kernel: most workgroups per CU (launch_c sizes the LDS pad)
@@ -161,6 +161,9 @@ hipError_t raise_dyn_lds(const void* fn, int bytes);
 
 hipError_t launch_sw_flow2(const LaunchCfg& cfg, const KParams& kp, hipStream_t stream);
 int flow2_waves_per_cu(int C);
+// workgroups per CU resident for the streamed flow2 kernel cfg selects (ring / slab
+// instantiation, LDS pad of cfg.f2_wgs); -1 on error (sw_flow2.hip)
+int flow2_stream_resident(const LaunchCfg& cfg, bool ring, bool slab);
 bool flow2_variant_exists(int C);
 
 hipError_t launch_sw_strip(const LaunchCfg& cfg, const KParams& kp, hipStream_t stream);

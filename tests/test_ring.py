@@ -38,17 +38,18 @@ def _pairs(rng):
     return out
 
 
-@pytest.mark.parametrize("stream", [0, 1])
-def test_ring_mode_matches_oracle(engine, oracle_mod, stream):
+def test_ring_mode_matches_oracle(engine, oracle_mod):
     """Forced ring mode on grids of 1, 2, 3 and 7 blocks (many rounds, the wrap
     ring used every round) and rings of 512 rows (rows wrap them several times),
-    staged and streamed row codes, default and G_INIT != G_EXT constants."""
-    rng = np.random.default_rng(91 + stream)
+    default and G_INIT != G_EXT constants.  Ring mode always runs the streamed-code
+    kernel (finalize_mode sets f2_stream with ring; variant bit 2); the staged
+    kernel and its loader wave are covered with linear edges
+    (test_gpu_parity.py::test_flow2_loader_wave)."""
+    rng = np.random.default_rng(91)
     pairs = _pairs(rng)
     engine.set_option("orient", 1)
     engine.set_option("mode", 5)
     engine.set_option("ring", 1)
-    engine.set_option("f2stream", stream)
     for prm in (engine.Params(), engine.Params(2, -3, 5, 2), engine.Params(3, -2, 4, 4)):
         op = oracle_mod.Params(prm.match, prm.mismatch, prm.gap_init, prm.gap_ext)
         exp = [oracle_mod.score_linear(a, b, op) for a, b in pairs]
@@ -61,6 +62,7 @@ def test_ring_mode_matches_oracle(engine, oracle_mod, stream):
                 st = engine.last_stats()
                 groups = ((len(a) - 1 + 62) // 63 + 3) // 4
                 assert st["mode"] == 5 and bool(st["variant"] & 4) == (groups > 1), st
+                assert groups == 1 or st["variant"] & 2, st   # ring mode streams the row codes
             assert got == exp, (prm, blocks, rows)
 
 

@@ -155,6 +155,38 @@ def test_slabs_threads_every_kernel(engine, oracle_mod, nslabs):
                 assert got[r] <= oracle_mod.score_slab(a, b, lo, hi, op)[0], (name, r, bounds)
 
 
+@pytest.mark.parametrize("nslabs", [2, 3])
+def test_slabs_ring_mode(engine, oracle_mod, nslabs):
+    """The ring + slab instantiation (sw_flow2_kernel<C, STREAM, RING, SLAB, LIN>), the
+    kernel the automatic plan runs for every C5 column slab: ring edges forced with
+    512-row rings and 3 blocks per slab (several rounds of ~8 groups, the wrap ring
+    every round, back-pressure since m > 512), with the linear-gap step, the affine
+    step on the same constants (linear = 0) and G_INIT != G_EXT constants."""
+    rng = np.random.default_rng(31 + nslabs)
+    engine.set_option("ring", 1)
+    engine.set_option("ring_rows", 512)
+    engine.set_option("blocks", 3)
+    try:
+        for prm, lin in ((engine.Params(), -1), (engine.Params(), 0), (engine.Params(2, -3, 5, 2), -1)):
+            engine.set_params(prm)
+            engine.set_option("linear", lin)
+            op = oracle_mod.Params(prm.match, prm.mismatch, prm.gap_init, prm.gap_ext)
+            for n, m in ((nslabs * 2000 + 77, 1500), (nslabs * 1800, 2100)):
+                a = _rand_dna(rng, n)
+                b = _similar(rng, a, m) if m < n else _rand_dna(rng, m)
+                exp = oracle_mod.score_linear(a, b, op)
+                got, bounds, stats = _run_threads(engine, a, b, nslabs, engine.SW_FLAG_DNA)
+                assert max(got) == exp, (prm, lin, n, m, got, exp, bounds)
+                for s in stats:
+                    assert s["mode"] == 5 and s["variant"] & 4 and s["variant"] & 2, s   # ring, streamed
+                    assert bool(s["variant"] & 8) == (lin != 0 and prm.gap_init == prm.gap_ext), s
+                    assert s["blocks"] == 3 and s["C"] == 64, s
+    finally:
+        engine.set_option("ring", -1)
+        engine.set_option("ring_rows", 4096)
+        engine.set_option("linear", -1)
+
+
 def test_slab_long_alignment_crosses_every_edge(engine):
     """An identical pair: the optimal alignment runs the whole diagonal through
     every slab edge, so any lost or stale hand-off lowers the score; three
