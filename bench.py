@@ -34,8 +34,10 @@ that applies is VALU issue, not HBM.  `roofline.achieved` = VALU lane-ops of one
 launch (rocprofv3 SQ_INSTS_VALU x 64, profiles/pmc_<workload>.json, valid only
 for the same libswmi355.so, checked by sha256) / the launch time measured here;
 `peak` = 256 CU x 4 SIMD x 64 lanes / 2 cycles x 2.4 GHz.  For the single pair
-`critical_path_frac` = (n+m-1) x the step time measured in this run (strip 0
-of a traced launch) / the launch time.  `traffic` = HBM bytes per launch from
+`critical_path_frac` = (m + 63 x strips) x the step time measured in this run
+(strip 0 of a traced launch) / the launch time: the wavefront's own bound, since
+strip s+1 cannot start a row sooner than 63 steps after strip s (n + m at one
+column per lane, m + n/2 at two).  `traffic` = HBM bytes per launch from
 the FETCH_SIZE / WRITE_SIZE passes of the same profile.
 """
 from __future__ import annotations
@@ -127,7 +129,8 @@ def cpu_baseline(kind: str, n: int, budget_s: float, params):
                 break
             rows = min(len(b), rows * 2)
         return {"value": cells / t_tot / 1e9, "unit": "GCUPS", "cores": 1, "kind": "port", "host": host,
-                "sample": "main.cpp SmithWatermanScore restated (full (m+1)x(n+1)x3 int32 matrices), "
+                "sample": "main.cpp SmithWatermanScore restated (full (m+1)x(n+1)x3 int32 matrices, one contiguous "
+                          "block instead of main.cpp's vector<vector<int>> rows: faster than the reference itself), "
                           "1 thread as in the reference, on row prefixes of the C2 pair up to %d x %d; %.1f s"
                           % (rows, len(a), t_tot)}
     if kind == "slab":
@@ -174,7 +177,7 @@ def profile_for(workload):
     return prof, os.path.relpath(path, ROOT)
 
 
-def roofline(workload, per_launch_cells, avg_kern_ms, step_ns=None, n=0, m=0):
+def roofline(workload, per_launch_cells, avg_kern_ms, step_ns=None, n=0, m=0, w2=False):
     prof, src = profile_for(workload)
     t = avg_kern_ms * 1e-3
     out = {"bound": "valu", "unit": "Tlane-ops/s", "peak": round(VALU_PEAK_TOPS, 2), "achieved": None, "frac": None,
@@ -196,9 +199,21 @@ def roofline(workload, per_launch_cells, avg_kern_ms, step_ns=None, n=0, m=0):
                   "note": "12 B/cell (int32 H, E, F, SURVEY 8d) is notional: the kernel keeps them on chip, so "
                           "algorithmic_frac can exceed 1; traffic_frac is the counted HBM bytes"}
     if step_ns:
+        # the wavefront's own bound at the measured step: strip s can start its row i no
+        # sooner than 63 steps after strip s-1 did (the lane skew), so the last strip ends
+        # after m + 63 * strips steps (W = 1: ~ n + m; two columns per lane: ~ m + n / 2)
+        strips = flow2_strips(n, w2)
         out["step_ns"] = round(step_ns, 3)
-        out["critical_path_frac"] = round((n + m - 1) * step_ns / (avg_kern_ms * 1e6), 4)
+        out["wavefront_steps"] = m + 63 * strips
+        out["critical_path_frac"] = round((m + 63 * strips) * step_ns / (avg_kern_ms * 1e6), 4)
     return out
+
+
+def flow2_strips(n, w2=False):
+    """Strips of the single-pair kernel (sw_internal.h flow2_strips / flow2_strips_w2)."""
+    if w2:
+        return 1 if n <= 128 else (n - 2 + 125) // 126
+    return 1 if n <= 64 else (n - 1 + 62) // 63
 
 
 def measure_step_ns(sw, torch, arena, offs_a, lens, offs_b, scores, sptr, N):
@@ -207,7 +222,7 @@ def measure_step_ns(sw, torch, arena, offs_a, lens, offs_b, scores, sptr, N):
     st = sw.last_stats()
     if st["mode"] != 5:
         return None
-    strips = max(1, (N - 1 + 62) // 63)
+    strips = flow2_strips(N, bool(st["variant"] & 16))
     trace = torch.zeros(16 * strips, dtype=torch.int64, device="cuda")
     sw.set_option("trace", trace.data_ptr())
     try:
@@ -521,7 +536,7 @@ def main():
             "parity": parity,
             "host_api": host_api,
             "roofline": roofline(workload if args.slab_of <= 1 else "slab_part", per_launch_cells, avg_kern_ms,
-                                 step_ns, cfg["N"], cfg["N"]),
+                                 step_ns, cfg["N"], cfg["N"], bool(st["variant"] & 16)),
         }
         if rccl is not None:
             out["rccl_world"] = rccl

@@ -57,7 +57,7 @@ std::mutex g_param_mu;
 Params g_params;
 
 std::atomic<long long> g_opt_W{0}, g_opt_C{0}, g_opt_bytes{0}, g_opt_timeout{30}, g_opt_blocks{0}, g_opt_orient{0},
-    g_opt_mode{-1}, g_opt_trace{0}, g_opt_duo_f16{1}, g_opt_f2stream{0}, g_opt_ring{-1}, g_opt_ring_rows{4096}, g_opt_f2_wgs{0},
+    g_opt_mode{-1}, g_opt_trace{0}, g_opt_duo_f16{1}, g_opt_f2stream{0}, g_opt_ring{-1}, g_opt_ring_rows{4096}, g_opt_f2_wgs{0}, g_opt_f2w{0},
     g_opt_linear{-1};
 
 // Longest sequence the engine takes: granule buffers of m rows keep m * 16 in the
@@ -193,6 +193,7 @@ struct Job {
     bool duo_f16 = false;        // MODE_DUO: max3 through v_pk_maximum3_f16 (duo_f16_fits)
     bool f2_stream = false;      // MODE_FLOW2: row codes streamed (rows too long to stage in LDS)
     bool ring = false;           // MODE_FLOW2, one pair: group edges through per-block rings (O(m) state)
+    bool f2w2 = false;           // MODE_FLOW2: two columns per lane (strips of 126 new columns, LIN step)
 };
 
 bool is_dna_byte(unsigned char c) { return c == 'A' || c == 'C' || c == 'G' || c == 'T'; }
@@ -336,13 +337,27 @@ bool flow2_staged(const Job& job, int max_m) {
     return g_opt_f2stream.load() == 0 && flow2_stage_bytes(max_m, job.C) <= flow2_stage_max(job.C);
 }
 
-// Re-plan a grouped job for MODE_FLOW2: strips of 64 columns overlapping by one.
-void plan_flow2(Job& job) {
+// Two columns per lane (sw_flow2.hip W2) whenever the linear-gap step runs (G_INIT ==
+// G_EXT, option linear not 0, C = 32 / 64); option f2w: 0 auto, 1 or 2 forced.
+// Measured (kernel ms, W = 1 -> 2): C2 3.46 -> 3.17 (half the strip hops and half the
+// wavefront's column term at a 25 instead of 17 ns step), C5 222 -> 181 (4.5 instead
+// of 5.5 VALU per 64 cells, throughput-bound).
+bool flow2_w2_wanted(const Job& job, const Params& p) {
+    const long long o = g_opt_f2w.load();
+    const bool lin = p.gap_init == p.gap_ext && g_opt_linear.load() != 0 && job.C != 16 &&
+                     (g_opt_C.load() == 0 || g_opt_C.load() == 32 || g_opt_C.load() == 64);
+    return lin && o != 1;
+}
+
+// Re-plan a grouped job for MODE_FLOW2: strips of 64 columns overlapping by one
+// (w2: 128 columns overlapping by two).
+void plan_flow2(Job& job, bool w2) {
     job.mode = MODE_FLOW2;
+    job.f2w2 = w2;
     uint64_t g = 0;
     for (size_t k = 0; k < job.pairs.size(); ++k) {
         PairDesc& d = job.pairs[k];
-        d.strips = flow2_strips(d.n);
+        d.strips = w2 ? flow2_strips_w2(d.n) : flow2_strips(d.n);
         d.bnd_off = g;
         g += (uint64_t)((d.strips + 3) / 4 - 1) * (uint64_t)d.m;
         job.item_base[k + 1] = job.item_base[k] + (d.strips + 3) / 4;
@@ -376,7 +391,7 @@ int finalize_mode(Job& job, const Params& prm) {
     }
     if (job.mode == MODE_FLOW2 || (g_opt_mode.load() < 0 && job.mode == MODE_CHAIN)) {
         if (flow2_fits(job, prm)) {
-            plan_flow2(job);
+            plan_flow2(job, flow2_w2_wanted(job, prm));
             job.f2_stream = job.ring || !flow2_staged(job, max_m);   // ring mode runs with streamed codes
             // ring mode (one pair of many groups per CU, C5): throughput-bound, so 64-row chunks
             // (half the per-chunk work per step) beat the shorter hand-off lag of 32 (C5 249 -> 220 ms)
@@ -442,7 +457,7 @@ int plan_slab(Job& job, int n, int m, bool dna, const Params& prm) {
         set_err("a column slab needs a grouped kernel (chain, flow or flow2), not mode %d", job.mode);
         return -1;
     }
-    return job.mode == MODE_FLOW2 ? 63 : 64 * job.W;
+    return job.mode == MODE_FLOW2 ? (job.f2w2 ? 126 : 63) : 64 * job.W;
 }
 
 // Alphabet of a slab call: stated by the caller, never scanned, because every
@@ -541,6 +556,7 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
         LaunchCfg probe{1, job.C, true, 0, MODE_FLOW2, 0};
         probe.f2_stream = true;
         probe.f2_lin = f2_lin;
+        probe.f2_w2 = job.f2w2;
         int fit = 0;
         for (;; --f2_wgs) {
             probe.f2_wgs = f2_wgs;
@@ -590,6 +606,11 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
     cfg.f2_stream = f2s;
     cfg.f2_wgs = f2_wgs;
     cfg.f2_lin = f2_lin;
+    cfg.f2_w2 = job.mode == MODE_FLOW2 && job.f2w2;
+    if (cfg.f2_w2 && !f2_lin) {   // the strips were cut for two columns per lane
+        set_err("flow2: two columns per lane needs the linear-gap step");
+        return -1;
+    }
     const int wpc = waves_per_cu(c, cfg);
     const int items = job.item_base[np];
     long long blocks = g_opt_blocks.load();
@@ -629,6 +650,11 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
         for (int r = 0; r < 4; ++r) w |= (unsigned)(((r == q ? prm.match : prm.mismatch) + prm.gap_init) & 0xFF) << (8 * r);
         kp.prof2[q] = w;
     }
+    for (int q = 0; q < 4; ++q) {   // flow2 W2 column B: signed bytes s(q, r)
+        unsigned w = 0;
+        for (int r = 0; r < 4; ++r) w |= (unsigned)((r == q ? prm.match : prm.mismatch) & 0xFF) << (8 * r);
+        kp.prof3[q] = w;
+    }
     for (int q = 0; q < 4; ++q) {   // duo: penalty bytes MATCH - s(r, q)
         unsigned w = 0;
         for (int r = 0; r < 4; ++r) w |= (unsigned)(r == q ? 0 : prm.match - prm.mismatch) << (8 * r);
@@ -660,7 +686,8 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
     t_stats.waves_per_cu = wpc;
     t_stats.items = items;
     t_stats.mode = job.mode;
-    t_stats.variant = (cfg.duo_f16 ? 1 : 0) | (cfg.f2_stream ? 2 : 0) | (job.ring ? 4 : 0) | (cfg.f2_lin ? 8 : 0);
+    t_stats.variant = (cfg.duo_f16 ? 1 : 0) | (cfg.f2_stream ? 2 : 0) | (job.ring ? 4 : 0) | (cfg.f2_lin ? 8 : 0) |
+                      (cfg.f2_w2 ? 16 : 0);
     t_stats.boundary_bytes = (long long)(job.bnd_granules * sizeof(Granule));
     c->last = s;
     return 0;
@@ -1133,6 +1160,9 @@ int sw_set_option(const char* key, long long v) {
     } else if (k == "f2_wgs") {   // flow2 streamed kernel: workgroups per CU, 0 = auto, 1..4
         if (v < 0 || v > 4) return -1;
         g_opt_f2_wgs = v;
+    } else if (k == "f2w") {   // flow2 columns per lane: 0 auto, 1, 2 (2: the linear-gap step only)
+        if (v < 0 || v > 2) return -1;
+        g_opt_f2w = v;
     } else if (k == "linear") {   // G_INIT == G_EXT: -1 auto (the linear-gap step), 0 = the affine step
         if (v < -1 || v > 0) return -1;
         g_opt_linear = v;
@@ -1166,6 +1196,7 @@ long long sw_get_option(const char* key) {
     if (k == "linear") return g_opt_linear;
     if (k == "f2_wgs") return g_opt_f2_wgs;
     if (k == "ring_rows") return g_opt_ring_rows;
+    if (k == "f2w") return g_opt_f2w;
     return -1;
 }
 

@@ -178,9 +178,18 @@ constexpr bool f2_loader() { return SW_F2_LOADER && !STREAM; }
 template <bool STREAM>
 constexpr int f2_threads() { return f2_loader<STREAM>() ? 320 : 256; }
 
-template <int C, bool STREAM, bool RING, bool SLAB, bool LIN>
+// W2: two columns per lane (LIN only).  Strip s covers columns [126s, 126s + 128),
+// lane l columns A = 126s + 2l and B = A + 1; strips overlap by two columns (lane 0
+// of strip s+1 recomputes lane 63's pair), so the hand-off is exactly W = 1's: the
+// outflow is lane 63's hgL_A = H(i, A - 1) - G, the left input of the next strip's
+// lane 0.  Inside a lane B's left neighbour is A (same row, same step); A's left is
+// lane l-1's B through the tied DPP-add.  10 VALU per step for 128 columns instead of
+// 5.5 for 64, and half the strips: the wavefront's column term and the number of
+// strip hops both halve.
+template <int C, bool STREAM, bool RING, bool SLAB, bool LIN, bool W2 = false>
 __global__ void __launch_bounds__(f2_threads<STREAM>()) sw_flow2_kernel(KParams kp) {
     static_assert(!(RING || SLAB) || STREAM, "ring and slab kernels stream the row codes");
+    static_assert(!W2 || LIN, "two columns per lane: the linear-gap step only");
     static_assert(C % 4 == 0 && 64 % C == 0 && 2 * C + 64 <= F2_R, "chunk");
     // STREAM ring: during chunk c the reads span rows [k0 + C - 63, k0 + 2C) and the
     // writes rows [k0 + 2C, k0 + 3C): no slot is rewritten while still read
@@ -195,7 +204,7 @@ __global__ void __launch_bounds__(f2_threads<STREAM>()) sw_flow2_kernel(KParams 
     constexpr int NT = f2_threads<STREAM>();
     constexpr int NR = LD ? 5 : 4;           // LDS rings: one per compute wave (+ the loader's)
     constexpr int CRB = F2_CR + C + 64;      // STREAM ring + mirror + per-lane sinks, bytes per wave
-    extern __shared__ unsigned char rc[];    // rc[row + 64]: 4..7 = A,C,G,T; 0 = no row (staged mode)
+    extern __shared__ __attribute__((aligned(16))) unsigned char rc[];   // rc[row + 64]: 4..7 = A,C,G,T; 0 = no row (staged mode)
     __shared__ __attribute__((aligned(16))) unsigned char cring[STREAM ? 4 : 1][STREAM ? CRB : 16];
     __shared__ int2 ring[NR][R];             // ring w: outflow rows of wave w (row r in slot r mod R)
     __shared__ int2 sink[NR][64];            // lanes that publish nothing write here
@@ -222,17 +231,27 @@ __global__ void __launch_bounds__(f2_threads<STREAM>()) sw_flow2_kernel(KParams 
         const __amdgpu_buffer_rsrc_t row_rsrc =
             __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned char*>(kp.seq + pd.row_off), 0, m, RSRC_FLAGS);
         if constexpr (!STREAM) {
-            const int nst = flow2_stage_bytes(m, C);
-            for (int i = tid * 4; i < nst; i += 4 * NT) {
-                unsigned w = 0;
+            // 16 rows per thread and load (the first group's staging delays the whole
+            // chain): rc[i .. i+16) = codes of rows i-64 .. i-49, 4 + code, 0 = no row
+            const int nst = flow2_stage_bytes(m, C);   // a multiple of 16
+            for (int i = tid * 16; i < nst; i += 16 * NT) {
+                const int row0 = i - 64;
+                u32x4 w = u32x4{0u, 0u, 0u, 0u};
+                if (row0 >= 0 && row0 + 16 <= m) {
+                    const u32x4 raw = __builtin_amdgcn_raw_buffer_load_b128(row_rsrc, (unsigned)row0, 0, 0);
 #pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const int row = i + j - 64;
-                    const bool live = row >= 0 && row < m;
-                    const unsigned ch = __builtin_amdgcn_raw_buffer_load_b8(row_rsrc, live ? (unsigned)row : OOR, 0, 0);
-                    w |= (live ? 4u + (unsigned)dna_code(ch) : 0u) << (8 * j);
+                    for (int q = 0; q < 4; ++q)
+                        w[q] = (((raw[q] >> 1) ^ (raw[q] >> 2)) & 0x03030303u) | 0x04040404u;   // dna_code per byte
+                } else if (row0 < m && row0 + 16 > 0) {   // the block holding row m-1: byte by byte
+#pragma unroll
+                    for (int j = 0; j < 16; ++j) {
+                        const int row = row0 + j;
+                        const bool live = row >= 0 && row < m;
+                        const unsigned ch = __builtin_amdgcn_raw_buffer_load_b8(row_rsrc, live ? (unsigned)row : OOR, 0, 0);
+                        w[j >> 2] |= (live ? 4u + (unsigned)dna_code(ch) : 0u) << (8 * (j & 3));
+                    }
                 }
-                *reinterpret_cast<unsigned*>(rc + i) = w;
+                *reinterpret_cast<u32x4*>(rc + i) = w;
             }
         }
         __syncthreads();
@@ -296,8 +315,10 @@ __global__ void __launch_bounds__(f2_threads<STREAM>()) sw_flow2_kernel(KParams 
         }
         const int strip = 4 * group + wave;
         if (strip >= pd.strips) continue;
-        const int col = 63 * strip + lane;
+        const int col = W2 ? 126 * strip + 2 * lane : 63 * strip + lane;
         const unsigned prof = col < pd.n ? kp.prof2[dna_code(kp.seq[pd.col_off + col])] : 0x80808080u;
+        // W2 column B takes its diagonal as H_A (not H_A - G): raw score bytes s
+        const unsigned profB = W2 && col + 1 < pd.n ? kp.prof3[dna_code(kp.seq[pd.col_off + col + 1])] : 0x80808080u;
         // a multi-GPU column slab: the first strip takes the previous slab's edge, the
         // last one hands its lane-62 column (the next slab's left neighbour) on
         const int ngroups = (pd.strips + 3) / 4;
@@ -334,6 +355,7 @@ __global__ void __launch_bounds__(f2_threads<STREAM>()) sw_flow2_kernel(KParams 
         long long tl[5] = {0, 0, 0, 0, 0};   // SW_TIMELINE: wall clock at chunks 1, 2, 3, 50, 1000
         // LIN keeps hgO clamped at 0 (see the step)
         int H = 0, E = 0, fh = -ge, hgO = LIN ? 0 : -go, L0 = -go, ehP = -ge, M = 0;
+        int HB = 0, hgOB = 0;                     // W2: column B of the lane
         int IOH = -go, IOE = -ge;                 // rotating I/O registers (see the step)
         // -G_INIT, -G_EXT kept in VGPRs (operands of the DPP-adds, which take no SGPR)
         int neggo, negge;
@@ -533,9 +555,13 @@ __global__ void __launch_bounds__(f2_threads<STREAM>()) sw_flow2_kernel(KParams 
                     newE = -ge;
                 }
                 // ---- scores of the chunk's rows: one v_perm_b32 per 4 rows
-                unsigned P[C / 4];
+                unsigned P[C / 4], PB[W2 ? C / 4 : 1];
 #pragma unroll
                 for (int u = 0; u < C / 4; ++u) P[u] = __builtin_amdgcn_perm(prof, 0x80808080u, D[u]);
+                if constexpr (W2) {
+#pragma unroll
+                    for (int u = 0; u < C / 4; ++u) PB[u] = __builtin_amdgcn_perm(profB, 0x80808080u, D[u]);
+                }
                 // take the inflow (and the scores) into registers before this chunk's LDS
                 // writes are issued, so the waits for them do not also wait for the writes
                 asm volatile("" : "+v"(newH), "+v"(newE));
@@ -621,9 +647,30 @@ __global__ void __launch_bounds__(f2_threads<STREAM>()) sw_flow2_kernel(KParams 
                         M = max(M, t);
                         L0 = hgL;
                     };
+                    auto step_lin2 = [&](auto b_c) __attribute__((always_inline)) {
+                        constexpr int b = decltype(b_c)::value;
+                        // 9 VALU for 128 cells.  Column A: as step_lin, with H_B of lane l-1 as
+                        // the left input.  Column B: diagonal = H_A of the last row taken
+                        // unshifted with the raw score byte (tB = H_A + s), left = max(H_A - G, 0)
+                        // of this row, which is hgO_A: the clamp only adds the 0 that
+                        // H = max(0, ...) has anyway, so no separate H_A - G is needed
+                        const int tA = L0 + sbyte<b>(P[j >> 2]);
+                        const int tB = H + sbyte<b>(PB[j >> 2]);
+                        int ioh = L0;
+                        const int hgL = rot_dpp_add(IOH, ioh, HB, neggo, hgOB);   // HB -> hgOB -> DPP
+                        IOH = ioh;
+                        H = vmax3(hgL, hgO, tA);
+                        hgO = sub_clamp0(H, go);
+                        HB = vmax3(hgO, hgOB, tB);
+                        hgOB = sub_clamp0(HB, go);
+                        M = vmax3(M, tA, tB);
+                        L0 = hgL;
+                    };
                     auto step = [&](auto b_c) __attribute__((always_inline)) {
                         constexpr int b = decltype(b_c)::value;
-                        if constexpr (LIN) {
+                        if constexpr (W2) {
+                            step_lin2(b_c);
+                        } else if constexpr (LIN) {
                             step_lin(b_c);
                         } else {
                             const int t = L0 + sbyte<b>(P[j >> 2]);
@@ -688,22 +735,22 @@ int flow2_dyn_lds(const LaunchCfg& cfg, int* lim) {
     return STREAM ? pad : std::max(flow2_stage_bytes(cfg.max_m, C), pad);
 }
 
-template <int C, bool STREAM, bool RING = false, bool SLAB = false, bool LIN = false>
+template <int C, bool STREAM, bool RING = false, bool SLAB = false, bool LIN = false, bool W2 = false>
 hipError_t prepare_c(const LaunchCfg& cfg, int* dyn) {
     int lim = 0;
     *dyn = flow2_dyn_lds<C, STREAM>(cfg, &lim);
     if (*dyn > lim) return hipErrorInvalidValue;
     if (*dyn > 64 * 1024)   // raise the dynamic-LDS limit (once per variant and device)
-        return raise_dyn_lds((const void*)sw_flow2_kernel<C, STREAM, RING, SLAB, LIN>, lim);
+        return raise_dyn_lds((const void*)sw_flow2_kernel<C, STREAM, RING, SLAB, LIN, W2>, lim);
     return hipSuccess;
 }
 
-template <int C, bool STREAM, bool RING = false, bool SLAB = false, bool LIN = false>
+template <int C, bool STREAM, bool RING = false, bool SLAB = false, bool LIN = false, bool W2 = false>
 hipError_t launch_c(const LaunchCfg& cfg, const KParams& kp, hipStream_t s) {
     int dyn = 0;
-    const hipError_t e = prepare_c<C, STREAM, RING, SLAB, LIN>(cfg, &dyn);
+    const hipError_t e = prepare_c<C, STREAM, RING, SLAB, LIN, W2>(cfg, &dyn);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL((sw_flow2_kernel<C, STREAM, RING, SLAB, LIN>), dim3(cfg.blocks), dim3(f2_threads<STREAM>()),
+    hipLaunchKernelGGL((sw_flow2_kernel<C, STREAM, RING, SLAB, LIN, W2>), dim3(cfg.blocks), dim3(f2_threads<STREAM>()),
                        (size_t)dyn, s, kp);
     return hipGetLastError();
 }
@@ -711,29 +758,30 @@ hipError_t launch_c(const LaunchCfg& cfg, const KParams& kp, hipStream_t s) {
 // Workgroups per CU the runtime will keep resident for the streamed instantiation a
 // launch of cfg would run (its registers, waves and the LDS of cfg.f2_wgs): what
 // ring mode's static deal must not exceed (every block resident).  -1 on error.
-template <int C, bool RING, bool SLAB, bool LIN>
+template <int C, bool RING, bool SLAB, bool LIN, bool W2>
 int resident_c(const LaunchCfg& cfg) {
     int dyn = 0, nb = 0;
-    if (prepare_c<C, true, RING, SLAB, LIN>(cfg, &dyn) != hipSuccess) return -1;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)sw_flow2_kernel<C, true, RING, SLAB, LIN>,
+    if (prepare_c<C, true, RING, SLAB, LIN, W2>(cfg, &dyn) != hipSuccess) return -1;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)sw_flow2_kernel<C, true, RING, SLAB, LIN, W2>,
                                                      f2_threads<true>(), (size_t)dyn) != hipSuccess)
         return -1;
     return nb;
 }
-template <int C, bool LIN>
+template <int C, bool LIN, bool W2 = false>
 int resident_v(const LaunchCfg& cfg, bool ring, bool slab) {
-    if (slab) return ring ? resident_c<C, true, true, LIN>(cfg) : resident_c<C, false, true, LIN>(cfg);
-    return ring ? resident_c<C, true, false, LIN>(cfg) : resident_c<C, false, false, LIN>(cfg);
+    if (slab) return ring ? resident_c<C, true, true, LIN, W2>(cfg) : resident_c<C, false, true, LIN, W2>(cfg);
+    return ring ? resident_c<C, true, false, LIN, W2>(cfg) : resident_c<C, false, false, LIN, W2>(cfg);
 }
 
 // the instantiation a launch needs: ring edges, slab edges, streamed or staged codes
-template <int C, bool LIN>
+template <int C, bool LIN, bool W2 = false>
 hipError_t launch_v(const LaunchCfg& cfg, const KParams& kp, hipStream_t s) {
     const bool ring = kp.ring_rows > 0, slab = kp.slab_in != nullptr || kp.slab_out != nullptr;
     if (slab)
-        return ring ? launch_c<C, true, true, true, LIN>(cfg, kp, s) : launch_c<C, true, false, true, LIN>(cfg, kp, s);
-    if (ring) return launch_c<C, true, true, false, LIN>(cfg, kp, s);
-    return cfg.f2_stream ? launch_c<C, true, false, false, LIN>(cfg, kp, s) : launch_c<C, false, false, false, LIN>(cfg, kp, s);
+        return ring ? launch_c<C, true, true, true, LIN, W2>(cfg, kp, s) : launch_c<C, true, false, true, LIN, W2>(cfg, kp, s);
+    if (ring) return launch_c<C, true, true, false, LIN, W2>(cfg, kp, s);
+    return cfg.f2_stream ? launch_c<C, true, false, false, LIN, W2>(cfg, kp, s)
+                         : launch_c<C, false, false, false, LIN, W2>(cfg, kp, s);
 }
 
 template <int C>
@@ -754,8 +802,15 @@ hipError_t launch_sw_flow2(const LaunchCfg& cfg, const KParams& kp, hipStream_t 
         // the linear-gap step (G_INIT == G_EXT) is built for 32-row (latency-bound pairs) and
         // 64-row chunks (ring mode, throughput-bound)
         case 16: return launch_v<16, false>(cfg, kp, stream);
-        case 32: return cfg.f2_lin ? launch_v<32, true>(cfg, kp, stream) : launch_v<32, false>(cfg, kp, stream);
-        case 64: return cfg.f2_lin ? launch_v<64, true>(cfg, kp, stream) : launch_v<64, false>(cfg, kp, stream);
+        // two columns per lane (cfg.f2_w2) with the linear-gap step only
+        case 32:
+            return cfg.f2_w2 && cfg.f2_lin ? launch_v<32, true, true>(cfg, kp, stream)
+                   : cfg.f2_lin            ? launch_v<32, true>(cfg, kp, stream)
+                                           : launch_v<32, false>(cfg, kp, stream);
+        case 64:
+            return cfg.f2_w2 && cfg.f2_lin ? launch_v<64, true, true>(cfg, kp, stream)
+                   : cfg.f2_lin            ? launch_v<64, true>(cfg, kp, stream)
+                                           : launch_v<64, false>(cfg, kp, stream);
         default: return hipErrorInvalidValue;
     }
 }
@@ -763,8 +818,14 @@ hipError_t launch_sw_flow2(const LaunchCfg& cfg, const KParams& kp, hipStream_t 
 int flow2_stream_resident(const LaunchCfg& cfg, bool ring, bool slab) {
     switch (cfg.C) {
         case 16: return resident_v<16, false>(cfg, ring, slab);
-        case 32: return cfg.f2_lin ? resident_v<32, true>(cfg, ring, slab) : resident_v<32, false>(cfg, ring, slab);
-        case 64: return cfg.f2_lin ? resident_v<64, true>(cfg, ring, slab) : resident_v<64, false>(cfg, ring, slab);
+        case 32:
+            return cfg.f2_w2 && cfg.f2_lin ? resident_v<32, true, true>(cfg, ring, slab)
+                   : cfg.f2_lin            ? resident_v<32, true>(cfg, ring, slab)
+                                           : resident_v<32, false>(cfg, ring, slab);
+        case 64:
+            return cfg.f2_w2 && cfg.f2_lin ? resident_v<64, true, true>(cfg, ring, slab)
+                   : cfg.f2_lin            ? resident_v<64, true>(cfg, ring, slab)
+                                           : resident_v<64, false>(cfg, ring, slab);
         default: return -1;
     }
 }

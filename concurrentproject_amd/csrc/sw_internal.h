@@ -75,6 +75,7 @@ struct KParams {
     int match, mismatch, gap_init, gap_ext;
     unsigned prof[4];             // DNA mode: per column code, 4 biased score bytes (row code 0..3)
     unsigned prof2[4];            // flow2 mode: per column code, 4 signed score bytes s + G_INIT (row code 0..3)
+    unsigned prof3[4];            // flow2 W2: per column code, 4 signed score bytes s (row code 0..3)
     unsigned pen[4];              // duo mode: per column code, 4 penalty bytes MATCH - s (row code 0..3)
     const DuoDesc* duos;          // duo mode: nduos descriptors (npairs counts duos)
     long long timeout_ticks;      // s_memrealtime ticks (100 MHz) before a spin gives up
@@ -128,6 +129,7 @@ struct LaunchCfg {
     int f2_wgs = 1;         // MODE_FLOW2 streamed: workgroups per CU (LDS pad sized to admit exactly this many)
     bool f2_lin = false;    // G_INIT == G_EXT, the exact linear-gap step: MODE_FLOW2 at C = 32 or 64 (sw_flow2.hip
                             // LIN) and MODE_DUO with duo_f16 (sw_kernels.hip StripDuo LIN)
+    bool f2_w2 = false;     // MODE_FLOW2 with f2_lin: two columns per lane (126 new columns per strip)
 };
 constexpr int F2_WGS_MAX = 4;   // flow2 streamed kernel: most workgroups per CU (launch_c sizes the LDS pad)
 
@@ -148,6 +150,8 @@ __host__ __device__ constexpr int flow_stage_max(int W, int C) { return LDS_PER_
 // codes of the pair are staged in LDS (one byte per row, 64 rows of border in
 // front, a chunk of prefetch behind).
 __host__ __device__ constexpr int flow2_strips(int n) { return n <= 64 ? 1 : (n - 1 + 62) / 63; }
+// two columns per lane (LaunchCfg::f2_w2): strip s covers columns [126s, 126s + 128)
+__host__ __device__ constexpr int flow2_strips_w2(int n) { return n <= 128 ? 1 : (n - 2 + 125) / 126; }
 __host__ __device__ constexpr int flow2_stage_bytes(int m, int C) {
     return (64 + ((m + 64 + C - 1) / C + 1) * C + 8 + 15) & ~15;
 }

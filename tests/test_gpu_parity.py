@@ -20,7 +20,7 @@ def _defaults(engine):
     engine.set_option("mode", -1)
     yield
     engine.set_params(engine.Params())
-    for k in ("W", "C", "bytes", "blocks", "orient"):
+    for k in ("W", "C", "bytes", "blocks", "orient", "f2w"):
         engine.set_option(k, 0)
     engine.set_option("mode", -1)
 
@@ -209,16 +209,21 @@ def test_flow2_ragged(engine, oracle_mod):
             engine.set_option("mode", 5)
             for C in (16, 32, 64):
                 engine.set_option("C", C)
-                # G_INIT == G_EXT at C = 32 / 64: the linear-gap step (auto) and the affine step (linear = 0)
-                for lin in ((-1, 0) if prm.gap_init == prm.gap_ext and C in (32, 64) else (-1,)):
+                # G_INIT == G_EXT at C = 32 / 64: the linear-gap step (auto) at two columns per lane (auto)
+                # and at one (f2w = 1), and the affine step (linear = 0)
+                lin_ok = prm.gap_init == prm.gap_ext and C in (32, 64)
+                for lin, f2w in (((-1, 0), (-1, 1), (0, 0)) if lin_ok else ((-1, 0),)):
                     engine.set_option("linear", lin)
+                    engine.set_option("f2w", f2w)
                     got = [engine.score(a, b, prm) for a, b in pairs]
-                    assert got == exp, (C, prm, lin)
+                    assert got == exp, (C, prm, lin, f2w)
                     st = engine.last_stats()
                     assert st["mode"] == 5
-                    assert bool(st["variant"] & 8) == (lin == -1 and prm.gap_init == prm.gap_ext and C in (32, 64)), st
-                    assert engine.score_batch(pairs, prm) == exp, (C, prm, lin)
+                    assert bool(st["variant"] & 8) == (lin == -1 and lin_ok), st
+                    assert bool(st["variant"] & 16) == (lin == -1 and lin_ok and f2w == 0), st
+                    assert engine.score_batch(pairs, prm) == exp, (C, prm, lin, f2w)
                 engine.set_option("linear", -1)
+                engine.set_option("f2w", 0)
             engine.set_option("C", 0)
             engine.set_option("blocks", 1)
             assert engine.score_batch(pairs, prm) == exp, prm
@@ -255,11 +260,14 @@ def test_flow2_loader_wave(engine, oracle_mod):
         for prm in (engine.Params(), engine.Params(2, -3, 5, 2)):
             op = oracle_mod.Params(prm.match, prm.mismatch, prm.gap_init, prm.gap_ext)
             exp = [oracle_mod.score_linear(a, b, op) for a, b in pairs]
-            for blocks in (1, 2, 3, 7, 0):
-                engine.set_option("blocks", blocks)
-                assert engine.score_batch(pairs, prm) == exp, (prm, blocks)
-                st = engine.last_stats()
-                assert st["mode"] == 5 and not st["variant"] & 2, st   # the staged kernel
+            for f2w in ((0, 1) if prm.gap_init == prm.gap_ext else (0,)):   # two / one column(s) per lane
+                engine.set_option("f2w", f2w)
+                for blocks in (1, 2, 3, 7, 0):
+                    engine.set_option("blocks", blocks)
+                    assert engine.score_batch(pairs, prm) == exp, (prm, blocks, f2w)
+                    st = engine.last_stats()
+                    assert st["mode"] == 5 and not st["variant"] & 2, st   # the staged kernel
+            engine.set_option("f2w", 0)
             assert [engine.score(a, b, prm) for a, b in pairs] == exp, prm
     finally:
         engine.set_option("mode", -1)
@@ -292,9 +300,12 @@ def test_flow2_streamed_rows(engine, oracle_mod):
             engine.set_option("mode", 5)
             for C in (16, 32, 64):
                 engine.set_option("C", C)
-                assert [engine.score(a, b, prm) for a, b in pairs] == exp, (C, prm)
-                assert engine.last_stats()["variant"] & 2
-                assert engine.score_batch(pairs, prm) == exp, (C, prm)
+                for f2w in ((0, 1) if prm.gap_init == prm.gap_ext and C > 16 else (0,)):
+                    engine.set_option("f2w", f2w)
+                    assert [engine.score(a, b, prm) for a, b in pairs] == exp, (C, prm, f2w)
+                    assert engine.last_stats()["variant"] & 2
+                    assert engine.score_batch(pairs, prm) == exp, (C, prm, f2w)
+                engine.set_option("f2w", 0)
             engine.set_option("C", 0)
             engine.set_option("mode", -1)
         engine.set_option("f2stream", 0)

@@ -7,7 +7,7 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 ACGT = np.frombuffer(b"ACGT", np.uint8)
-OPTS = ("W", "C", "blocks", "orient", "f2stream", "f2_wgs")
+OPTS = ("W", "C", "blocks", "orient", "f2stream", "f2_wgs", "f2w")
 
 
 @pytest.fixture(autouse=True)
@@ -60,8 +60,12 @@ def test_ring_mode_matches_oracle(engine, oracle_mod):
             for a, b in pairs:
                 got.append(engine.score(a, b, prm))
                 st = engine.last_stats()
-                groups = ((len(a) - 1 + 62) // 63 + 3) // 4
+                n = len(a)
+                strips = ((n - 2 + 125) // 126 if n > 128 else 1) if st["variant"] & 16 else (n - 1 + 62) // 63
+                groups = (strips + 3) // 4
                 assert st["mode"] == 5 and bool(st["variant"] & 4) == (groups > 1), st
+                # two columns per lane exactly when the linear-gap step runs (G_INIT == G_EXT)
+                assert bool(st["variant"] & 16) == (prm.gap_init == prm.gap_ext), st
                 assert groups == 1 or st["variant"] & 2, st   # ring mode streams the row codes
             assert got == exp, (prm, blocks, rows)
 
@@ -78,14 +82,17 @@ def test_ring_matches_linear_edges(engine):
     assert st["variant"] & 4 and st["boundary_bytes"] < 64 << 20, st
 
 
+@pytest.mark.parametrize("f2w", [1, 2])
 @pytest.mark.parametrize("wgs", [1, 2, 3, 4])
-def test_ring_round_change(engine, wgs):
-    """1588 groups over 256..1024 resident blocks (2..7 rounds): a block starts its
-    next round while the consumer of its ring, one hop behind, still reads the last
-    rows of the previous one.  The back-pressure check also covers a round's first
-    R rows (before it did not, and N = 400000 at 2 workgroups per CU timed out).
-    Ring edges at 1..4 workgroups per CU against write-once edges."""
+def test_ring_round_change(engine, wgs, f2w):
+    """1588 groups at one column per lane (794 at two) over 256..1024 resident blocks
+    (1..7 rounds): a block starts its next round while the consumer of its ring, one
+    hop behind, still reads the last rows of the previous one.  The back-pressure
+    check also covers a round's first R rows (before it did not, and N = 400000 at 2
+    workgroups per CU timed out).  Ring edges at 1..4 workgroups per CU against
+    write-once edges."""
     a, b = engine.gen_pair(400000, 400000)
+    engine.set_option("f2w", f2w)
     engine.set_option("f2_wgs", wgs)
     engine.set_option("ring", 0)
     lin = engine.score(a, b)
@@ -94,7 +101,9 @@ def test_ring_round_change(engine, wgs):
     st = engine.last_stats()
     import torch
     cus = torch.cuda.get_device_properties(0).multi_processor_count
-    assert st["variant"] & 4 and st["blocks"] == min(1588, wgs * cus), st
+    items = st["items"]   # 4-strip groups: 1588 at one column per lane, 794 at two
+    assert items == (1588 if f2w == 1 else 794) and bool(st["variant"] & 16) == (f2w == 2), st
+    assert st["variant"] & 4 and st["blocks"] == min(items, wgs * cus), st
     assert got == lin > 0, (got, lin)
 
 

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Per-strip timeline of the flow kernels (mode 4, or 5 = flow2) on one long pair.
 
-    python tools/trace_flow.py N C [W] [n_cols] [mode]
+    python tools/trace_flow.py N C [W] [n_cols] [mode] [f2w]
 
 Each strip records s_memrealtime (100 MHz) at start, when its first inflow
 chunk arrived, and at the end, plus the number of failed progress polls.
@@ -24,16 +24,23 @@ def main():
     W = int(sys.argv[3]) if len(sys.argv) > 3 else 1
     ncol = int(sys.argv[4]) if len(sys.argv) > 4 else N
     mode = int(sys.argv[5]) if len(sys.argv) > 5 else 4
+    f2w = int(sys.argv[6]) if len(sys.argv) > 6 else 0   # flow2 columns per lane (option f2w)
     torch.cuda.set_device(0)
     a, b = sw.gen_pair(N, N)
     a = a[:ncol]
     arena = torch.from_numpy(np.concatenate([a, b])).cuda()
     scores = torch.zeros(1, dtype=torch.int32, device="cuda")
-    strips = (ncol + 64 * W - 1) // (64 * W) if mode != 5 else max(1, (ncol - 1 + 62) // 63)
+    if mode != 5:
+        strips = (ncol + 64 * W - 1) // (64 * W)
+    elif f2w == 2:
+        strips = 1 if ncol <= 128 else (ncol - 2 + 125) // 126
+    else:
+        strips = max(1, (ncol - 1 + 62) // 63)
     trace = torch.zeros(16 * strips, dtype=torch.int64, device="cuda")
     sw.set_option("mode", mode)
     sw.set_option("W", W)
     sw.set_option("C", C)
+    sw.set_option("f2w", f2w)
     s = torch.cuda.current_stream()
     for it in range(3):
         if it == 2:
@@ -49,7 +56,7 @@ def main():
     lag = np.diff(first)
     ingroup = np.array([(k + 1) % 4 != 0 for k in range(strips - 1)], dtype=bool)
     run_ns = end - first
-    steps = N + 64 * W - 1
+    steps = N + 64 * W - 1 if mode != 5 else N + 63
     out = {
         "N": N, "ncol": ncol, "C": C, "W": W, "score": int(scores.item()), "strips": strips,
         "total_ms": float(end.max()) / 1e6,
