@@ -845,6 +845,9 @@ __device__ __forceinline__ unsigned codes_duo(unsigned raw0, unsigned raw1, int 
     return 0x0C000C00u | (s1 << 16) | s0;
 }
 
+#ifndef SW_DUO_SLACK
+#define SW_DUO_SLACK 0   // chunks a duo strip lets its producer lead by before it starts
+#endif
 template <int W, int C, bool M3, bool LIN>
 __device__ void strip_pass_duo(const KParams& kp, const DuoDesc& d, const int strip, const int lane) {
     constexpr int SW = 64 * W;
@@ -865,6 +868,14 @@ __device__ void strip_pass_duo(const KParams& kp, const DuoDesc& d, const int st
         __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned char*>(kp.seq + d.row_off[1]), 0, d.m[1], RSRC_FLAGS);
     const int nchunks = (m + SW - 1 + C - 1) / C;
     bool failed = false;
+    if constexpr (SW_DUO_SLACK > 0) {
+        // start only once the producer strip has published chunk SW_DUO_SLACK: the lead keeps
+        // every later chunk's granules (loaded one chunk ahead) published before they are read
+        if (has_in && SW_DUO_SLACK * C < m) {
+            u32x4 g0 = fetch_granules<C>(in_e, SW_DUO_SLACK * C, lane, m);
+            await_granules<C>(kp, in_e, g0, SW_DUO_SLACK * C, lane, m, strip, failed);
+        }
+    }
     unsigned raw0_nxt = fetch_raw(r0, 0, lane, C, d.m[0]), raw1_nxt = fetch_raw(r1, 0, lane, C, d.m[1]);
     u32x4 g_nxt = has_in ? fetch_granules<C>(in_e, 0, lane, m) : u32x4{0u, 0u, 0u, 0u};
     for (int c = 0; c < nchunks; ++c) {

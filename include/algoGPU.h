@@ -93,7 +93,8 @@ int sw_stream_status(void* stream);
  * R slab maxima (an all-reduce(MAX) of one int).  dist.ColumnSlabs drives it.
  *
  * sw_slab_bounds: R+1 column bounds; every slab but the last is a multiple of
- *   the kernel's column quantum (returned, > 0; 63 or 64*W).  flags must say
+ *   the kernel's column quantum (returned, > 0; 126 at two flow2 columns per lane,
+ *   63 at one, 64*W for chain / flow).  flags must say
  *   SW_FLAG_DNA or SW_FLAG_BYTES (all ranks must plan the same kernel).
  * sw_score_slab_device: one slab, sequences resident in device memory:
  *   columns d_arena[col_off, col_off+n), rows d_arena[row_off, row_off+m).
@@ -160,11 +161,14 @@ void sw_db_close(sw_db* db);
  *   "duo16"    1 = (default) packed duos take max3 through v_pk_maximum3_f16 when every
  *              value stays below 0x7C00 (MATCH*(min(n,m)+1) <= 31743), 0 = u16 max only
  *   "linear"   -1 = (default) the exact linear-gap step when G_INIT == G_EXT
- *              (flow2 C = 32, f16 duos), 0 = always the affine step
+ *              (flow2 C = 32 or 64, f16 duos), 0 = always the affine step
+ *   "f2w"      flow2 columns per lane: 0 = (default) two whenever the linear-gap
+ *              step runs, one otherwise; 1 = always one; 2 = two (linear-gap step only)
  *   "ring"     -1 = (default) ring edges for a single flow2 pair whose linear edges
  *              would exceed 1 GB, 0 = never, 1 = always (one pair per launch)
  *   "ring_rows" rows per within-round ring, a power of two in [512, 2^20] (4096)
- *   "f2_wgs"   flow2 streamed kernel: workgroups per CU, 0 = auto, 1..4
+ *   "f2_wgs"   flow2 streamed kernel: workgroups per CU, 0 = auto, 1..4 (ring mode:
+ *              lowered to what the runtime reports resident for its kernel)
  *   "f2stream" 1 = flow2 streams the row codes even when they fit in LDS (tests)
  *   "trace"    device address of a 16 x u64 per-strip trace buffer, 0 = off (tools)
  * Returns 0, or -1 for an unknown key / bad value. */
@@ -180,7 +184,8 @@ typedef struct {
     long long boundary_bytes;
     int mode;
     int variant;            /* bit 0: duo max3 via v_pk_maximum3_f16; bit 1: flow2 streams row codes;
-                               bit 2: flow2 ring edges; bit 3: the linear-gap step */
+                               bit 2: flow2 ring edges; bit 3: the linear-gap step;
+                               bit 4: flow2 two columns per lane */
 } sw_stats;
 int sw_last_stats(sw_stats* out);
 
