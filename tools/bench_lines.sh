@@ -1,0 +1,8 @@
+# The round's bench lines for C2 (default auto line), C3 (batch) and C5 (slab workload, one GPU),
+# taken after tools/pmc_summary.py has stamped profiles/pmc_*.json for this build, so every line's
+# roofline carries the counter-derived `achieved` / `frac` (GPU box).
+set -e
+mkdir -p gpurun_out/lines
+timeout -k 10 240 python bench.py --steps 10 --warmup 2 > gpurun_out/lines/bench_c2.json 2> gpurun_out/lines/bench_c2.err
+timeout -k 10 240 python bench.py --workload batch --steps 5 --warmup 1 > gpurun_out/lines/bench_c3.json 2> gpurun_out/lines/bench_c3.err
+timeout -k 10 240 python bench.py --workload slab --steps 3 --warmup 1 --cpu-seconds 10 > gpurun_out/lines/bench_c5.json 2> gpurun_out/lines/bench_c5.err
