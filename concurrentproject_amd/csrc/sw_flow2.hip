@@ -45,7 +45,8 @@ constexpr int F2_R = 256;   // ring rows per link (power of two, >= 2C + 64)
 #define SW_F2_GPREF 1       // cross-workgroup granules are loaded this many chunks ahead
 #endif
 #ifndef SW_F2_SPEC
-#define SW_F2_SPEC 0        // >0: the next chunk's inflow is read speculatively after SW_F2_SPEC/4 of a chunk
+#define SW_F2_SPEC 0        // >0: the next chunk's LDS inflow is read speculatively SW_F2_SPEC steps (a multiple of 4)
+                            // before the chunk ends (C2 W2: off 3.153, 4 steps 3.26, 8 steps 3.146, 12 steps 3.21 ms)
 #endif
 #ifndef SW_F2_GPOS
 #define SW_F2_GPOS 1        // chunk c+SW_F2_GPREF's granules are loaded after SW_F2_GPOS/4 of chunk c's steps
@@ -194,6 +195,7 @@ __global__ void __launch_bounds__(f2_threads<STREAM>()) sw_flow2_kernel(KParams 
     // STREAM ring: during chunk c the reads span rows [k0 + C - 63, k0 + 2C) and the
     // writes rows [k0 + 2C, k0 + 3C): no slot is rewritten while still read
     static_assert(!STREAM || 3 * C + 63 <= F2_CR, "code ring");
+    static_assert(SW_F2_SPEC % 4 == 0 && SW_F2_SPEC < C, "speculative inflow read");
     static_assert(!SW_F2_HALFLDS || (SW_F2_SPEC == 0 && SW_F2_HALFIN_AHEAD % 4 == 0 && SW_F2_HALFIN_AHEAD <= C / 2),
                   "half-chunk LDS links");
     // rows per LDS hand-off: the consumer needs rows [k0, k0 + HL) at the start of a
@@ -624,7 +626,7 @@ __global__ void __launch_bounds__(f2_threads<STREAM>()) sw_flow2_kernel(KParams 
                         }
                     }
                     if constexpr (IN == FLOW_LDS && SW_F2_SPEC > 0) {
-                        if (j == SW_F2_SPEC * C / 4) {   // speculative read of the next chunk's inflow
+                        if (j == C - SW_F2_SPEC) {   // speculative read of the next chunk's inflow
                             spec_avail = lds_load(&prod[in_w]);
                             compiler_fence();
                             spec_v = in_ring[(k0 + C + (lane & (C - 1))) & (R - 1)];
@@ -654,6 +656,12 @@ __global__ void __launch_bounds__(f2_threads<STREAM>()) sw_flow2_kernel(KParams 
                         // unshifted with the raw score byte (tB = H_A + s), left = max(H_A - G, 0)
                         // of this row, which is hgO_A: the clamp only adds the 0 that
                         // H = max(0, ...) has anyway, so no separate H_A - G is needed
+                        // The maxima stay inline asm (vmax3) although the compiler pads a read of an
+                        // asm result in the next instruction with s_nop 0 (it assumes a 16-bit dst_sel
+                        // write).  Compiler-visible maxima removed C2's 16-20 nops per 32 steps but the
+                        // kernel got slower (3.15 -> 3.30 ms: a lone wave's 4-step body times the same
+                        // either way, tools/ubench_w2seq.hip, and the rest of the chunk scheduled worse),
+                        // and the streamed kernels grew from 93 to 135 VGPRs (ring mode needs <= 128).
                         const int tA = L0 + sbyte<b>(P[j >> 2]);
                         const int tB = H + sbyte<b>(PB[j >> 2]);
                         int ioh = L0;

@@ -646,6 +646,10 @@ __device__ __forceinline__ unsigned as32(u16x2 v) { return __builtin_bit_cast(un
 __device__ __forceinline__ u16x2 vmax2(u16x2 a, u16x2 b) { return __builtin_elementwise_max(a, b); }
 __device__ __forceinline__ u16x2 vsubs2(u16x2 a, u16x2 b) { return __builtin_elementwise_sub_sat(a, b); }
 __device__ __forceinline__ u16x2 splat2(int v) { return u16x2{(unsigned short)v, (unsigned short)v}; }
+// a + b of both halves as ONE 32-bit add (VOP2 v_add_u32: about half the issue cost of
+// v_pk_add_u16 on gfx950, tools/ubench_bank.hip) -- exact when no low-half sum reaches
+// 2^16, which duo_fits guarantees for A = H + MATCH <= MATCH*min(n,m) + MATCH <= 65535
+__device__ __forceinline__ u16x2 add2(u16x2 a, u16x2 b) { return as16(as32(a) + as32(b)); }
 
 // v_pk_maximum3_f16 as an UNSIGNED 16-bit max3 (gfx950): for halves in [0, 0x7BFF]
 // -- sign clear, no Inf/NaN encodings, f16 denormals preserved (the HIP default
@@ -728,7 +732,9 @@ struct StripDuo {
                                              const u16x2 ma2, const u16x2 gom2) {
         const u16x2 aL0 = as16((unsigned)dpp_shr1((int)IOA, (int)as32(aPrev[W - 1])));
         constexpr int s0 = (W - S % W) % W;
-        r[s0] = (unsigned)dpp_shr1((int)IOR, (int)r[s0]);
+        const unsigned ior = IOR;
+        IOR = (unsigned)__builtin_amdgcn_mov_dpp((int)ior, DPP_WAVE_SHL1, 0xF, 0xF, true);
+        r[s0] = (unsigned)dpp_shr1((int)ior, (int)r[s0]);
         const u16x2 hgL0 = vsubs2(aL0, gom2);
         u16x2 tOdd = splat2(0);
 #pragma unroll
@@ -749,12 +755,11 @@ struct StripDuo {
                 H = vmax2(vmax2(t, hgL), hg[p]);
                 M = vmax2(M, t);
             }
-            aCur[p] = H + ma2;
+            aCur[p] = add2(H, ma2);
             hg[p] = vsubs2(H, go2);
         }
         L0 = aL0;
         IOA = (unsigned)__builtin_amdgcn_update_dpp((int)as32(aCur[W - 1]), (int)IOA, DPP_WAVE_SHL1, 0xF, 0xF, false);
-        IOR = (unsigned)__builtin_amdgcn_mov_dpp((int)IOR, DPP_WAVE_SHL1, 0xF, 0xF, true);
     }
 
     template <int S>
@@ -767,7 +772,9 @@ struct StripDuo {
         const u16x2 aL0 = as16((unsigned)dpp_shr1((int)IOA, (int)as32(aPrev[W - 1])));
         const u16x2 ehL0 = as16((unsigned)dpp_shr1((int)IOE, (int)as32(eh[W - 1])));
         constexpr int s0 = (W - S % W) % W;     // slot of position 0 (= last step's position W-1)
-        r[s0] = (unsigned)dpp_shr1((int)IOR, (int)r[s0]);
+        const unsigned ior = IOR;   // rotated first: the slot DPP then takes the old IOR (no copy)
+        IOR = (unsigned)__builtin_amdgcn_mov_dpp((int)ior, DPP_WAVE_SHL1, 0xF, 0xF, true);
+        r[s0] = (unsigned)dpp_shr1((int)ior, (int)r[s0]);
         const u16x2 hgL0 = vsubs2(aL0, gom2);   // H - G_INIT of the left neighbour, from its A
         u16x2 tOdd = splat2(0);                 // M3: t of position p+1, folded with p's into M
 #pragma unroll
@@ -791,7 +798,7 @@ struct StripDuo {
                 H = vmax2(vmax2(t, E), F);
                 M = vmax2(M, t);
             }
-            aCur[p] = H + ma2;
+            aCur[p] = add2(H, ma2);
             hg[p] = vsubs2(H, go2);
             eh[p] = vsubs2(E, ge2);
             fh[p] = vsubs2(F, ge2);
@@ -801,7 +808,6 @@ struct StripDuo {
         // source, keeps the 'old' operand: this step's right-edge outflow (no select)
         IOA = (unsigned)__builtin_amdgcn_update_dpp((int)as32(aCur[W - 1]), (int)IOA, DPP_WAVE_SHL1, 0xF, 0xF, false);
         IOE = (unsigned)__builtin_amdgcn_update_dpp((int)as32(eh[W - 1]), (int)IOE, DPP_WAVE_SHL1, 0xF, 0xF, false);
-        IOR = (unsigned)__builtin_amdgcn_mov_dpp((int)IOR, DPP_WAVE_SHL1, 0xF, 0xF, true);
     }
 
     // steps K, K+1, ... of an unrolled group of U = max(W, 2): slot rotation by S = K mod W,
