@@ -177,7 +177,36 @@ def profile_for(workload):
     return prof, os.path.relpath(path, ROOT)
 
 
-def roofline(workload, per_launch_cells, avg_kern_ms, step_ns=None, n=0, m=0, w2=False):
+def issue_bound(prof, avg_kern_ms, waves_per_simd):
+    """The kernel's VALU issue-time bound from the measured per-class issue costs
+    (tools/issue_model.py, profiles/r03_ubench_issue_classes.jsonl): the profiled
+    SQ_INSTS_VALU priced at the ns per SIMD of its chunk loop's instruction mix at this
+    launch's waves per SIMD, spread over the 1024 SIMDs.  The guide's 2-cycle peak above
+    holds for VOP1/VOP2-class instructions only; 3-source VOP3, VOP3P, DPP and SDWA
+    forms issue at ~1.75-1.9 ns per SIMD however many waves share it."""
+    mix = (prof or {}).get("valu_mix")
+    if not mix or not prof.get("valu_insts_per_launch"):
+        return None
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import issue_model
+    table = issue_model.cost_table()
+    ns = issue_model.issue_ns(mix["mix"], waves_per_simd, table)
+    bound_ms = prof["valu_insts_per_launch"] * ns / (256 * 4) / 1e6
+    return {"bound_ms": round(bound_ms, 4), "frac": round(bound_ms / avg_kern_ms, 4), "waves_per_simd": waves_per_simd,
+            "ns_per_valu_per_simd": round(ns, 4), "mix": {k: round(v, 4) for k, v in mix["mix"].items()},
+            "source": "tools/issue_model.py + profiles/r03_ubench_issue_classes.jsonl"}
+
+
+def resident_waves_per_simd(st, torch):
+    """Waves per SIMD of a launch: its workgroups' waves (4; the staged flow2 kernel 5)
+    up to the occupancy the engine planned with (sw_last_stats waves_per_cu)."""
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    wpb = 5 if st["mode"] == 5 and not st["variant"] & 2 else 4
+    waves = min(st["blocks"] * wpb, cus * max(1, st["waves_per_cu"]))
+    return max(1, round(waves / (cus * 4)))
+
+
+def roofline(workload, per_launch_cells, avg_kern_ms, step_ns=None, n=0, m=0, w2=False, waves_per_simd=None):
     prof, src = profile_for(workload)
     t = avg_kern_ms * 1e-3
     out = {"bound": "valu", "unit": "Tlane-ops/s", "peak": round(VALU_PEAK_TOPS, 2), "achieved": None, "frac": None,
@@ -188,6 +217,8 @@ def roofline(workload, per_launch_cells, avg_kern_ms, step_ns=None, n=0, m=0, w2
         out["frac"] = round(ops / t / 1e12 / VALU_PEAK_TOPS, 4)
         out["valu_lane_ops_per_launch"] = ops
         out["valu_insts_per_cell"] = round(prof["valu_insts_per_launch"] * 64 / per_launch_cells, 3)
+    if prof is not None and waves_per_simd:
+        out["issue"] = issue_bound(prof, avg_kern_ms, waves_per_simd)
     if prof is not None:
         out["traffic"] = prof.get("hbm_bytes_per_launch")
         if prof.get("clock_ghz"):
@@ -499,18 +530,24 @@ def main():
                      if defaults and len(ref) >= len(bsc) == 1024 * world else "unchecked",
                      "kernel": {3: "duo", 1: "pairwg"}.get(bst["mode"], bst["mode"]),
                      "dtype": "u16x2 (packed, exact: scores < 2^16)" if bst["mode"] == 3 else "int32",
-                     "roofline": roofline("batch", bcells, bk)}
+                     "roofline": roofline("batch", bcells, bk, waves_per_simd=resident_waves_per_simd(bst, torch))}
         if extra is not None and world == 1:
-            # the same batch on the int32 pair-per-workgroup kernel (no 16-bit packing)
-            sw.set_option("mode", 1)
-            try:
-                it, ik, isc, _, ist = run_batch(sw, torch, None, 1, 0, 8192, 1024, 2, 1)
-                extra["int32_kernel"] = {"kernel": "pairwg", "kernel_ms_per_launch": round(ik, 4),
-                                         "kernel_gcups": round(bcells / (ik * 1e-3) / 1e9, 3),
-                                         "parity": ("ok" if isc == ref[:len(isc)] else "MISMATCH")
-                                         if defaults and len(ref) >= 1024 else "unchecked"}
-            finally:
-                sw.set_option("mode", args.mode if args.mode >= 0 else -1)
+            # the same batch on the int32 kernels (no 16-bit packing): the flow2 step with a
+            # pair per workgroup, which the engine picks for batches whose scores need int32,
+            # and the pair-per-workgroup strip kernel it replaced there
+            for key, mode, pwg, name in (("int32_kernel", 5, 1, "flow2 pair per workgroup"),
+                                         ("pairwg_kernel", 1, -1, "pairwg")):
+                sw.set_option("mode", mode)
+                sw.set_option("f2pwg", pwg)
+                try:
+                    it, ik, isc, _, ist = run_batch(sw, torch, None, 1, 0, 8192, 1024, 2, 1)
+                    extra[key] = {"kernel": name, "kernel_ms_per_launch": round(ik, 4),
+                                  "kernel_gcups": round(bcells / (ik * 1e-3) / 1e9, 3),
+                                  "parity": ("ok" if isc == ref[:len(isc)] else "MISMATCH")
+                                  if defaults and len(ref) >= 1024 else "unchecked"}
+                finally:
+                    sw.set_option("mode", args.mode if args.mode >= 0 else -1)
+                    sw.set_option("f2pwg", -1)
 
     value = cells_job * args.steps / t_max / 1e9
     if rank == 0:
@@ -536,7 +573,8 @@ def main():
             "parity": parity,
             "host_api": host_api,
             "roofline": roofline(workload if args.slab_of <= 1 else "slab_part", per_launch_cells, avg_kern_ms,
-                                 step_ns, cfg["N"], cfg["N"], bool(st["variant"] & 16)),
+                                 step_ns, cfg["N"], cfg["N"], bool(st["variant"] & 16),
+                                 waves_per_simd=None if workload == "pair" else resident_waves_per_simd(st, torch)),
         }
         if rccl is not None:
             out["rccl_world"] = rccl

@@ -217,30 +217,38 @@ __device__ __forceinline__ void compiler_fence() { __asm__ __volatile__("" ::: "
 
 // where a wave's strip inflow comes from / its outflow goes (flow kernels)
 // (FLOW_PEER: a slab edge, granules to / from another GPU, system scope)
-enum : int { FLOW_NONE = 0, FLOW_GRANULE = 1, FLOW_LDS = 2, FLOW_PEER = 3 };
+// (FLOW_WRAP: flow2 pair per workgroup, wave 3 -> wave 0 of the next round through an
+// LDS buffer holding a whole round's rows, without back-pressure)
+enum : int { FLOW_NONE = 0, FLOW_GRANULE = 1, FLOW_LDS = 2, FLOW_PEER = 3, FLOW_WRAP = 4 };
 // the cache policy of a granule hand-off kind
 __host__ __device__ constexpr int flow_aux(int kind) { return kind == FLOW_PEER ? AUX_SYS : AUX_SC1; }
 __host__ __device__ constexpr bool flow_granule(int kind) { return kind == FLOW_GRANULE || kind == FLOW_PEER; }
 
 // A strip's (inflow, outflow) kinds as compile-time constants: calls f(IN{}, OUT{}),
 // so every hand-off loop is instantiated per role with unconditional memory ops.
-// PEER = false (a kernel that never runs a slab): the 9 combinations without
-// FLOW_PEER.  The 16-combination body measured 8 % slower on C2 even though the
-// peer roles never ran there (code layout), so slab launches get their own kernel.
-template <bool PEER, class F>
+// SET = KINDS_GRANULE (a kernel that never runs a slab): the 9 combinations without
+// FLOW_PEER.  The 16-combination body (KINDS_PEER) measured 8 % slower on C2 even
+// though the peer roles never ran there (code layout), so slab launches get their own
+// kernel.  KINDS_LDS: NONE, LDS and WRAP (the pair-per-workgroup kernel).
+enum : int { KINDS_GRANULE = 0, KINDS_PEER = 1, KINDS_LDS = 2 };
+template <int SET, class F>
 __device__ __forceinline__ void dispatch_kinds(int in_kind, int out_kind, F&& f) {
+    constexpr bool PEER = SET == KINDS_PEER, GRAN = SET != KINDS_LDS;
     using K0 = std::integral_constant<int, FLOW_NONE>;
     using K1 = std::integral_constant<int, FLOW_GRANULE>;
     using K2 = std::integral_constant<int, FLOW_LDS>;
     using K3 = std::integral_constant<int, FLOW_PEER>;
+    using K4 = std::integral_constant<int, FLOW_WRAP>;
     auto outs = [&](auto in_c) __attribute__((always_inline)) {
         if (out_kind == FLOW_LDS) f(in_c, K2{});
-        else if (out_kind == FLOW_GRANULE) f(in_c, K1{});
+        else if (!GRAN && out_kind == FLOW_WRAP) f(in_c, std::conditional_t<GRAN, K0, K4>{});
+        else if (GRAN && out_kind == FLOW_GRANULE) f(in_c, std::conditional_t<GRAN, K1, K0>{});
         else if (PEER && out_kind == FLOW_PEER) f(in_c, std::conditional_t<PEER, K3, K1>{});
         else f(in_c, K0{});
     };
     if (in_kind == FLOW_LDS) outs(K2{});
-    else if (in_kind == FLOW_GRANULE) outs(K1{});
+    else if (!GRAN && in_kind == FLOW_WRAP) outs(std::conditional_t<GRAN, K0, K4>{});
+    else if (GRAN && in_kind == FLOW_GRANULE) outs(std::conditional_t<GRAN, K1, K0>{});
     else if (PEER && in_kind == FLOW_PEER) outs(std::conditional_t<PEER, K3, K1>{});
     else outs(K0{});
 }

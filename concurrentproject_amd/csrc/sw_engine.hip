@@ -57,7 +57,7 @@ std::mutex g_param_mu;
 Params g_params;
 
 std::atomic<long long> g_opt_W{0}, g_opt_C{0}, g_opt_bytes{0}, g_opt_timeout{30}, g_opt_blocks{0}, g_opt_orient{0},
-    g_opt_mode{-1}, g_opt_trace{0}, g_opt_duo_f16{1}, g_opt_f2stream{0}, g_opt_ring{-1}, g_opt_ring_rows{4096}, g_opt_f2_wgs{0}, g_opt_f2w{0},
+    g_opt_mode{-1}, g_opt_trace{0}, g_opt_duo_f16{1}, g_opt_f2stream{0}, g_opt_ring{-1}, g_opt_ring_rows{4096}, g_opt_f2_wgs{0}, g_opt_f2w{0}, g_opt_f2pwg{-1},
     g_opt_linear{-1};
 
 // Longest sequence the engine takes: granule buffers of m rows keep m * 16 in the
@@ -194,6 +194,7 @@ struct Job {
     bool f2_stream = false;      // MODE_FLOW2: row codes streamed (rows too long to stage in LDS)
     bool ring = false;           // MODE_FLOW2, one pair: group edges through per-block rings (O(m) state)
     bool f2w2 = false;           // MODE_FLOW2: two columns per lane (strips of 126 new columns, LIN step)
+    bool pwg = false;            // MODE_FLOW2 batch: a pair per workgroup (sw_flow2.hip PWG)
 };
 
 bool is_dna_byte(unsigned char c) { return c == 'A' || c == 'C' || c == 'G' || c == 'T'; }
@@ -350,19 +351,22 @@ bool flow2_w2_wanted(const Job& job, const Params& p) {
 }
 
 // Re-plan a grouped job for MODE_FLOW2: strips of 64 columns overlapping by one
-// (w2: 128 columns overlapping by two).
-void plan_flow2(Job& job, bool w2) {
+// (w2: 128 columns overlapping by two).  pwg: one item per pair, whose workgroup runs all
+// of its strips with LDS hand-offs only (no granule edges).
+void plan_flow2(Job& job, bool w2, bool pwg = false) {
     job.mode = MODE_FLOW2;
     job.f2w2 = w2;
+    job.pwg = pwg;
     uint64_t g = 0;
     for (size_t k = 0; k < job.pairs.size(); ++k) {
         PairDesc& d = job.pairs[k];
         d.strips = w2 ? flow2_strips_w2(d.n) : flow2_strips(d.n);
         d.bnd_off = g;
-        g += (uint64_t)((d.strips + 3) / 4 - 1) * (uint64_t)d.m;
-        job.item_base[k + 1] = job.item_base[k] + (d.strips + 3) / 4;
+        if (!pwg) g += (uint64_t)((d.strips + 3) / 4 - 1) * (uint64_t)d.m;
+        job.item_base[k + 1] = job.item_base[k] + (pwg ? 1 : (d.strips + 3) / 4);
     }
     job.bnd_granules = g;
+    if (pwg) return;
     // Ring mode (sw_flow2.hip, KParams::ring_rows): one pair whose write-once group
     // edges would take more than RING_AUTO_BYTES (C5: 69.8 GB), or when forced.  Stream
     // positions are 32-bit and may wrap: slots are taken mod a power of two <= 2^24,
@@ -377,6 +381,24 @@ void plan_flow2(Job& job, bool w2) {
     }
 }
 
+// The pair-per-workgroup kernel keeps a round's rows of its longest pair in LDS: at least
+// `wgs` such workgroups must fit a CU (automatic choice: 2, m up to ~8.5k rows).
+bool pwg_fits(const Job& job, int wgs) {
+    int max_m = 0;
+    for (const PairDesc& d : job.pairs) max_m = std::max(max_m, d.m);
+    return flow2_pwg_wgs(max_m, 64) >= wgs;
+}
+
+// A batch on the pair-per-workgroup flow2 kernel: W = 1 strips, 64-row chunks, streamed
+// codes; two columns per lane with the linear-gap step (G_INIT == G_EXT), else the affine
+// step at one column per lane.
+void plan_pwg(Job& job, const Params& prm) {
+    job.W = 1;
+    job.C = 64;
+    plan_flow2(job, flow2_w2_wanted(job, prm), true);
+    job.f2_stream = true;
+}
+
 int finalize_mode(Job& job, const Params& prm) {
     int max_m = 0;
     for (const PairDesc& d : job.pairs) max_m = std::max(max_m, d.m);
@@ -388,6 +410,15 @@ int finalize_mode(Job& job, const Params& prm) {
         Job w1 = job;
         plan(w1, 1, pick_C(1), true, MODE_CHAIN);
         if (flow2_fits(w1, prm)) job = w1;
+    }
+    if (job.mode == MODE_FLOW2 && job.pairs.size() > 1 && g_opt_f2pwg.load() == 1) {
+        Job w1 = job;   // a forced flow2 batch, a pair per workgroup (W = 1 strips, C = 64)
+        plan(w1, 1, 64, false, MODE_FLOW2);
+        if (flow2_fits(w1, prm) && pwg_fits(w1, 1)) {
+            job = w1;
+            plan_pwg(job, prm);
+            return 0;
+        }
     }
     if (job.mode == MODE_FLOW2 || (g_opt_mode.load() < 0 && job.mode == MODE_CHAIN)) {
         if (flow2_fits(job, prm)) {
@@ -429,6 +460,16 @@ int finalize_mode(Job& job, const Params& prm) {
         if (forced_duo) {
             set_err("duo mode needs an {A,C,G,T} batch whose scores fit 16 bits (MATCH*min(n,m)+MATCH <= 65535)");
             return -1;
+        }
+        // scores that need int32: the flow2 step with a pair per workgroup when it applies
+        // (C3-shaped batch on int32: pairwg 18.9 ms -> flow2 PWG, sw_flow2.hip)
+        if (g_opt_f2pwg.load() != 0 && job.pairs.size() > 1 && job.dna) {
+            Job w1 = job;
+            plan(w1, 1, 64, false, MODE_CHAIN);
+            if (flow2_fits(w1, prm) && pwg_fits(w1, 2)) {
+                job = w1;
+                plan_pwg(job, prm);
+            }
         }
     }
     return 0;
@@ -530,6 +571,8 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
     // with many strip groups per CU (C5) is throughput-bound, and more waves per
     // SIMD hide each other's issue latency (sw_flow2.hip launch_c sizes the LDS pad)
     const bool f2s = job.mode == MODE_FLOW2 && (job.f2_stream || job.ring || edge != nullptr);
+    int max_m_all = 0;
+    for (const PairDesc& d : job.pairs) max_m_all = std::max(max_m_all, d.m);
     // Measured (kernel ms, ring | linear edges, 1/2/3/4 per CU):
     //   N = 2^17 (520 groups)   9.8 9.7 9.6 9.6   | 9.4 10.8 12.5 12.8
     //   N = 2^18 (1040)         32.4 25.2 26.2 26.4 | 31.7 26.3 34.2 32.1
@@ -540,7 +583,11 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
     if (f2s) {
         const long long o = g_opt_f2_wgs.load();
         const int per_cu = job.item_base[np] / c->cus;
-        f2_wgs = o > 0 ? (int)o : job.ring ? std::min(F2_WGS_MAX, std::max(1, per_cu / 2)) : per_cu >= 4 ? 2 : 1;
+        f2_wgs = o > 0           ? (int)o
+                 : job.ring      ? std::min(F2_WGS_MAX, std::max(1, per_cu / 2))
+                 : job.pwg       ? std::min({F2_WGS_MAX, std::max(1, per_cu), flow2_pwg_wgs(max_m_all, job.C)})
+                 : per_cu >= 4   ? 2
+                                 : 1;
     }
     // G_INIT == G_EXT: the exact linear-gap step (sw_flow2.hip LIN), unless disabled
     const bool f2_lin = ((job.mode == MODE_FLOW2 && (job.C == 32 || job.C == 64)) ||
@@ -607,6 +654,7 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
     cfg.f2_wgs = f2_wgs;
     cfg.f2_lin = f2_lin;
     cfg.f2_w2 = job.mode == MODE_FLOW2 && job.f2w2;
+    cfg.f2_pwg = job.mode == MODE_FLOW2 && job.pwg;
     if (cfg.f2_w2 && !f2_lin) {   // the strips were cut for two columns per lane
         set_err("flow2: two columns per lane needs the linear-gap step");
         return -1;
@@ -687,7 +735,7 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
     t_stats.items = items;
     t_stats.mode = job.mode;
     t_stats.variant = (cfg.duo_f16 ? 1 : 0) | (cfg.f2_stream ? 2 : 0) | (job.ring ? 4 : 0) | (cfg.f2_lin ? 8 : 0) |
-                      (cfg.f2_w2 ? 16 : 0);
+                      (cfg.f2_w2 ? 16 : 0) | (cfg.f2_pwg ? 32 : 0);
     t_stats.boundary_bytes = (long long)(job.bnd_granules * sizeof(Granule));
     c->last = s;
     return 0;
@@ -1163,6 +1211,9 @@ int sw_set_option(const char* key, long long v) {
     } else if (k == "f2w") {   // flow2 columns per lane: 0 auto, 1, 2 (2: the linear-gap step only)
         if (v < 0 || v > 2) return -1;
         g_opt_f2w = v;
+    } else if (k == "f2pwg") {   // int32 DNA batches on flow2, a pair per workgroup: -1 auto, 0 off, 1 forced
+        if (v < -1 || v > 1) return -1;
+        g_opt_f2pwg = v;
     } else if (k == "linear") {   // G_INIT == G_EXT: -1 auto (the linear-gap step), 0 = the affine step
         if (v < -1 || v > 0) return -1;
         g_opt_linear = v;
@@ -1197,6 +1248,7 @@ long long sw_get_option(const char* key) {
     if (k == "f2_wgs") return g_opt_f2_wgs;
     if (k == "ring_rows") return g_opt_ring_rows;
     if (k == "f2w") return g_opt_f2w;
+    if (k == "f2pwg") return g_opt_f2pwg;
     return -1;
 }
 

@@ -187,10 +187,17 @@ constexpr int f2_threads() { return f2_loader<STREAM>() ? 320 : 256; }
 // lane l-1's B through the tied DPP-add.  10 VALU per step for 128 columns instead of
 // 5.5 for 64, and half the strips: the wavefront's column term and the number of
 // strip hops both halve.
-template <int C, bool STREAM, bool RING, bool SLAB, bool LIN, bool W2 = false>
+//
+// PWG (batches of pairs whose scores need int32, sw_engine.hip plan_flow2): a workgroup
+// claims a whole pair and its 4 waves run all of its strips in rounds (wave w: strips w,
+// w + 4, ...), every hand-off through the LDS rings (wave 3 -> wave 0 of the next round
+// included): no granules, no cross-workgroup waits, so any grid size works.  Streamed codes.
+template <int C, bool STREAM, bool RING, bool SLAB, bool LIN, bool W2 = false, bool PWG = false>
 __global__ void __launch_bounds__(f2_threads<STREAM>()) sw_flow2_kernel(KParams kp) {
     static_assert(!(RING || SLAB) || STREAM, "ring and slab kernels stream the row codes");
     static_assert(!W2 || LIN, "two columns per lane: the linear-gap step only");
+    static_assert(!PWG || (STREAM && !RING && !SLAB), "pair per workgroup: streamed codes, LDS links only");
+    static_assert(!PWG || (SW_F2_SPEC == 0 && !SW_F2_HALFLDS), "pair per workgroup: whole-chunk LDS reads");
     static_assert(C % 4 == 0 && 64 % C == 0 && 2 * C + 64 <= F2_R, "chunk");
     // STREAM ring: during chunk c the reads span rows [k0 + C - 63, k0 + 2C) and the
     // writes rows [k0 + 2C, k0 + 3C): no slot is rewritten while still read
@@ -223,7 +230,7 @@ __global__ void __launch_bounds__(f2_threads<STREAM>()) sw_flow2_kernel(KParams 
         __syncthreads();   // every wave is done with the previous item
         const int item = __builtin_amdgcn_readfirstlane(s_item);
         if (item >= kp.total_items) return;
-        const int pi = find_pair(kp, item);
+        const int pi = PWG ? item : find_pair(kp, item);
         const PairDesc pd = load_pair(kp, pi);
         const int m = pd.m;
         const int group = item - kp.item_base[pi];
@@ -315,418 +322,455 @@ __global__ void __launch_bounds__(f2_threads<STREAM>()) sw_flow2_kernel(KParams 
             }
             continue;
         }
-        const int strip = 4 * group + wave;
-        if (strip >= pd.strips) continue;
-        const int col = W2 ? 126 * strip + 2 * lane : 63 * strip + lane;
-        const unsigned prof = col < pd.n ? kp.prof2[dna_code(kp.seq[pd.col_off + col])] : 0x80808080u;
-        // W2 column B takes its diagonal as H_A (not H_A - G): raw score bytes s
-        const unsigned profB = W2 && col + 1 < pd.n ? kp.prof3[dna_code(kp.seq[pd.col_off + col + 1])] : 0x80808080u;
-        // a multi-GPU column slab: the first strip takes the previous slab's edge, the
-        // last one hands its lane-62 column (the next slab's left neighbour) on
-        const int ngroups = (pd.strips + 3) / 4;
-        const int in_kind = wave > 0 || (LD && strip > 0) ? FLOW_LDS
-                            : strip > 0                   ? FLOW_GRANULE
-                            : kp.slab_in != nullptr       ? FLOW_PEER
-                                                          : FLOW_NONE;
-        const int in_w = wave > 0 ? wave - 1 : 4;   // the ring an LDS inflow comes from (4: the loader's)
-        const int out_kind = strip + 1 >= pd.strips ? (kp.slab_out != nullptr ? FLOW_PEER : FLOW_NONE)
-                             : wave < 3           ? FLOW_LDS
-                                                  : FLOW_GRANULE;
-        const Edge in_e = group_edge(kp, pd, group - 1, ngroups);
-        const Edge out_e = group_edge(kp, pd, group, ngroups);
-        // ring mode: the consumer of ring j reports the positions it has consumed in
-        // ring_cons[j]; the producer never overwrites a slot whose position is not
-        // consumed yet (back-pressure).  The wrap ring holds >= m rows and needs none:
-        // its consumer (block 0, round k+1) has read row r of round k before the chain
-        // of round k+1 lets block G-1 produce row r again.
-        unsigned* cons_in = nullptr;
-        unsigned* bp_word = nullptr;
-        if constexpr (RING) {
-            const int G = (int)gridDim.x;
-            if (group > 0 && (group - 1) % G != G - 1) cons_in = kp.ring_cons + ((group - 1) % G) * RING_CONS_STRIDE;
-            if (group < ngroups - 1 && group % G != G - 1) bp_word = kp.ring_cons + (group % G) * RING_CONS_STRIDE;
-        }
-        const bool cons_live = cons_in != nullptr;
-        const __amdgpu_buffer_rsrc_t cons_rsrc = __builtin_amdgcn_make_buffer_rsrc(cons_live ? cons_in : nullptr, 0,
-                                                                                    cons_live ? 4 : 0, RSRC_FLAGS);
-        const long long t_start = (long long)__builtin_amdgcn_s_memrealtime();
-        bool failed = false;
-        long long t_first = t_start;
-        int nslow = 0;   // chunks whose inflow took the slow path (trace only)
-        int fail_in = -1, fail_bp = -1;   // RING trace: chunk whose inflow / back-pressure wait timed out
-        long long tl[5] = {0, 0, 0, 0, 0};   // SW_TIMELINE: wall clock at chunks 1, 2, 3, 50, 1000
-        // LIN keeps hgO clamped at 0 (see the step)
-        int H = 0, E = 0, fh = -ge, hgO = LIN ? 0 : -go, L0 = -go, ehP = -ge, M = 0;
-        int HB = 0, hgOB = 0;                     // W2: column B of the lane
-        int IOH = -go, IOE = -ge;                 // rotating I/O registers (see the step)
-        // -G_INIT, -G_EXT kept in VGPRs (operands of the DPP-adds, which take no SGPR)
-        int neggo, negge;
-        asm volatile("v_mov_b32 %0, %1" : "=v"(neggo) : "s"(-go));
-        asm volatile("v_mov_b32 %0, %1" : "=v"(negge) : "s"(-ge));
-        // progress words are written by every lane: lane 0 to the word, the others to sinks
-        // (no exec-mask branch, so the compiler counts LDS operations exactly)
-        int* const prod_out = lane == 0 ? &prod[wave] : &psink[wave][lane];
-        int* const cons_out = lane == 0 ? &cons[wave] : &psink[wave][lane];
-        int2* const in_ring = ring[in_w < NR ? in_w : 0];
-        int2* const out_ring = ring[wave];
-        // per-lane code address: lane l reads rows k - l .. k - l + 3 (unaligned dword)
-        const unsigned char* const code_base = rc + 64 - lane;
-        // STREAM: this wave's code ring; codes of chunk cc's rows from their raw bytes
-        unsigned char* const cr = cring[STREAM ? wave : 0];
-        auto raw_of = [&](const int cc) __attribute__((always_inline)) {
-            const int row = cc * C + lane;
-            return __builtin_amdgcn_raw_buffer_load_b8(row_rsrc, lane < C && row < m ? (unsigned)row : OOR, 0, 0);
-        };
-        auto put_codes = [&](const unsigned raw, const int cc) __attribute__((always_inline)) {
-            const int row = cc * C + lane;
-            const bool wl = lane < C;
-            const unsigned char code = (unsigned char)(wl && row < m ? 4u + (unsigned)dna_code(raw) : 0u);
-            const int s1 = wl ? ((row + 64) & (F2_CR - 1)) : F2_CR + C + lane;
-            const int s2 = wl && s1 < C ? F2_CR + s1 : F2_CR + C + lane;
-            cr[s1] = code;
-            cr[s2] = code;
-        };
-        // where lane l's reads of chunk k0's rows start (STREAM: in the ring)
-        auto code_at = [&](const int k0) __attribute__((always_inline)) -> const unsigned char* {
-            if constexpr (STREAM) return cr + ((k0 + 64 - lane) & (F2_CR - 1));
-            else return code_base + k0;
-        };
-        // STREAM: the raw bytes of chunk c+2, loaded during chunk c-1: one register
-        // instead of a rotated pair (copying an in-flight load's destination makes the
-        // compiler wait for that load; C5 430 -> 422 ms)
-        unsigned rq0 = 0;
-        if constexpr (STREAM) {
-            for (int i = lane; i < CRB / 4; i += 64) reinterpret_cast<unsigned*>(cr)[i] = 0u;   // rows < 0: no row
-            const unsigned r0 = raw_of(0), r1 = raw_of(1);
-            put_codes(r0, 0);
-            put_codes(r1, 1);
-            rq0 = raw_of(2);
-        }
+        // PWG: this workgroup runs every strip of the pair, wave w the strips w, w + 4, ...
+        // (one per round); wave 3 hands off to wave 0 of the next round through LDS too.
+        // Positions on every link: row r of round k at k * span + 128 + r (span = the
+        // rows a round spans, so rounds never share a position, and a producer's first
+        // publishes of round k need only what its consumer has read of round k - 1).
+        const int nrounds = PWG ? (pd.strips + 3) / 4 : 1;
+        const int span = PWG ? nloc * C : 0;
+        for (int round = 0; round < nrounds; ++round) {
+            const int strip = PWG ? 4 * round + wave : 4 * group + wave;
+            if (strip >= pd.strips) break;
+            const int pb_out = PWG ? round * span + 128 : 0;                       // positions this strip publishes at
+            const int pb_in = PWG ? (wave > 0 ? round : round - 1) * span + 128 : 0;   // and reads at
+            const int col = W2 ? 126 * strip + 2 * lane : 63 * strip + lane;
+            const unsigned prof = col < pd.n ? kp.prof2[dna_code(kp.seq[pd.col_off + col])] : 0x80808080u;
+            // W2 column B takes its diagonal as H_A (not H_A - G): raw score bytes s
+            const unsigned profB = W2 && col + 1 < pd.n ? kp.prof3[dna_code(kp.seq[pd.col_off + col + 1])] : 0x80808080u;
+            // a multi-GPU column slab: the first strip takes the previous slab's edge, the
+            // last one hands its lane-62 column (the next slab's left neighbour) on
+            const int ngroups = (pd.strips + 3) / 4;
+            const int in_kind = PWG ? (strip == 0 ? FLOW_NONE : wave == 0 ? FLOW_WRAP : FLOW_LDS)
+                                : wave > 0 || (LD && strip > 0) ? FLOW_LDS
+                                : strip > 0                     ? FLOW_GRANULE
+                                : kp.slab_in != nullptr         ? FLOW_PEER
+                                                                : FLOW_NONE;
+            // the ring an LDS inflow comes from (4: the loader's; PWG wave 0: wave 3's, last round)
+            const int in_w = wave > 0 ? wave - 1 : PWG ? 3 : 4;
+            const int out_kind = strip + 1 >= pd.strips ? (kp.slab_out != nullptr ? FLOW_PEER : FLOW_NONE)
+                                 : wave < 3             ? FLOW_LDS
+                                 : PWG                  ? FLOW_WRAP
+                                                        : FLOW_GRANULE;
+            // PWG: the wave 3 -> wave 0 link holds a whole round in the dynamic LDS (the rows
+            // of round k - 1 stay until wave 0 of round k has read them: wave 3 writes row x
+            // of round k only after wave 0 of round k has computed row x, so it needs no
+            // back-pressure, which would close a cycle of waits 0 -> 1 -> 2 -> 3 -> 0)
+            int2* const wrapbuf = reinterpret_cast<int2*>(rc);
+            const Edge in_e = group_edge(kp, pd, group - 1, ngroups);
+            const Edge out_e = group_edge(kp, pd, group, ngroups);
+            // ring mode: the consumer of ring j reports the positions it has consumed in
+            // ring_cons[j]; the producer never overwrites a slot whose position is not
+            // consumed yet (back-pressure).  The wrap ring holds >= m rows and needs none:
+            // its consumer (block 0, round k+1) has read row r of round k before the chain
+            // of round k+1 lets block G-1 produce row r again.
+            unsigned* cons_in = nullptr;
+            unsigned* bp_word = nullptr;
+            if constexpr (RING) {
+                const int G = (int)gridDim.x;
+                if (group > 0 && (group - 1) % G != G - 1) cons_in = kp.ring_cons + ((group - 1) % G) * RING_CONS_STRIDE;
+                if (group < ngroups - 1 && group % G != G - 1) bp_word = kp.ring_cons + (group % G) * RING_CONS_STRIDE;
+            }
+            const bool cons_live = cons_in != nullptr;
+            const __amdgpu_buffer_rsrc_t cons_rsrc = __builtin_amdgcn_make_buffer_rsrc(cons_live ? cons_in : nullptr, 0,
+                                                                                        cons_live ? 4 : 0, RSRC_FLAGS);
+            const long long t_start = (long long)__builtin_amdgcn_s_memrealtime();
+            bool failed = false;
+            long long t_first = t_start;
+            int nslow = 0;   // chunks whose inflow took the slow path (trace only)
+            int fail_in = -1, fail_bp = -1;   // RING trace: chunk whose inflow / back-pressure wait timed out
+            long long tl[5] = {0, 0, 0, 0, 0};   // SW_TIMELINE: wall clock at chunks 1, 2, 3, 50, 1000
+            // LIN keeps hgO clamped at 0 (see the step)
+            int H = 0, E = 0, fh = -ge, hgO = LIN ? 0 : -go, L0 = -go, ehP = -ge, M = 0;
+            int HB = 0, hgOB = 0;                     // W2: column B of the lane
+            int IOH = -go, IOE = -ge;                 // rotating I/O registers (see the step)
+            // -G_INIT, -G_EXT kept in VGPRs (operands of the DPP-adds, which take no SGPR)
+            int neggo, negge;
+            asm volatile("v_mov_b32 %0, %1" : "=v"(neggo) : "s"(-go));
+            asm volatile("v_mov_b32 %0, %1" : "=v"(negge) : "s"(-ge));
+            // progress words are written by every lane: lane 0 to the word, the others to sinks
+            // (no exec-mask branch, so the compiler counts LDS operations exactly)
+            int* const prod_out = lane == 0 ? &prod[wave] : &psink[wave][lane];
+            int* const cons_out = lane == 0 ? &cons[wave] : &psink[wave][lane];
+            int2* const in_ring = ring[in_w < NR ? in_w : 0];
+            int2* const out_ring = ring[wave];
+            // per-lane code address: lane l reads rows k - l .. k - l + 3 (unaligned dword)
+            const unsigned char* const code_base = rc + 64 - lane;
+            // STREAM: this wave's code ring; codes of chunk cc's rows from their raw bytes
+            unsigned char* const cr = cring[STREAM ? wave : 0];
+            auto raw_of = [&](const int cc) __attribute__((always_inline)) {
+                const int row = cc * C + lane;
+                return __builtin_amdgcn_raw_buffer_load_b8(row_rsrc, lane < C && row < m ? (unsigned)row : OOR, 0, 0);
+            };
+            auto put_codes = [&](const unsigned raw, const int cc) __attribute__((always_inline)) {
+                const int row = cc * C + lane;
+                const bool wl = lane < C;
+                const unsigned char code = (unsigned char)(wl && row < m ? 4u + (unsigned)dna_code(raw) : 0u);
+                const int s1 = wl ? ((row + 64) & (F2_CR - 1)) : F2_CR + C + lane;
+                const int s2 = wl && s1 < C ? F2_CR + s1 : F2_CR + C + lane;
+                cr[s1] = code;
+                cr[s2] = code;
+            };
+            // where lane l's reads of chunk k0's rows start (STREAM: in the ring)
+            auto code_at = [&](const int k0) __attribute__((always_inline)) -> const unsigned char* {
+                if constexpr (STREAM) return cr + ((k0 + 64 - lane) & (F2_CR - 1));
+                else return code_base + k0;
+            };
+            // STREAM: the raw bytes of chunk c+2, loaded during chunk c-1: one register
+            // instead of a rotated pair (copying an in-flight load's destination makes the
+            // compiler wait for that load; C5 430 -> 422 ms)
+            unsigned rq0 = 0;
+            if constexpr (STREAM) {
+                for (int i = lane; i < CRB / 4; i += 64) reinterpret_cast<unsigned*>(cr)[i] = 0u;   // rows < 0: no row
+                const unsigned r0 = raw_of(0), r1 = raw_of(1);
+                put_codes(r0, 0);
+                put_codes(r1, 1);
+                rq0 = raw_of(2);
+            }
 
-        auto flow_loop = [&](auto in_c, auto out_c) __attribute__((always_inline)) {
-            constexpr int IN = decltype(in_c)::value, OUT = decltype(out_c)::value;
-            constexpr int AIN = flow_aux(IN), AOUT = flow_aux(OUT);
-            // granule prefetch queue: gq[i] holds the loads for chunk c + i (issued SW_F2_GPREF chunks ahead)
-            u32x4 gq[SW_F2_GPREF];
-#pragma unroll
-            for (int i = 0; i < SW_F2_GPREF; ++i)
-                gq[i] = flow_granule(IN) ? fetch_granules<C, AIN>(in_e, i * C, lane, m) : u32x4{0u, 0u, 0u, 0u};
-            unsigned D[C / 4];
-            load_codes<C>(D, code_at(0));
-            int cons_seen = 0;
-            int h_avail = 0;                     // SW_F2_HALFLDS: the mid-chunk inflow read
-            int2 h_v = make_int2(0, 0);
-            int spec_avail = -1;                 // progress word read with spec_v (-1: none)
-            int2 spec_v = make_int2(0, 0);
-            // granule outflow at step k0 (chunk start, or mid-chunk with SW_F2_HALFPUB):
-            // lane L >= 64 - C holds row k0 - 128 + L; with half-chunk publishing only
-            // lanes >= 64 - C/2 are new
-            unsigned bp_seen = 0;   // ring mode: last value read of the consumer's progress word
-            auto publish_granules_half = [&](const int k0) __attribute__((always_inline)) {
-                const int row_out = k0 - 128 + lane;
-                constexpr int LO = SW_F2_HALFPUB ? 64 - C / 2 : 64 - C;
-                const bool st = lane >= LO && row_out >= 0 && row_out < m;
-                if (RING && bp_word != nullptr) {
-                    // rows <= k0 - 65 go out: positions <= pos0 + k0 - 65 - R must be consumed.
-                    // Also at the start of a round (k0 - 64 <= R): the slots then still hold the
-                    // previous round's last rows, which the consumer (one hop behind, in that
-                    // round) may not have read yet; `need` is then below pos0, in wrap-safe
-                    // unsigned arithmetic, and in round 0 below 0, so always met.
-                    const unsigned need = out_e.pos0 + (unsigned)(k0 - 64 - kp.ring_rows);
-                    if ((int)(bp_seen - need) < 0) {
-                        bp_seen = __builtin_amdgcn_readfirstlane(
-                            __hip_atomic_load(bp_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-                        while ((int)(bp_seen - need) < 0) {
-                            __builtin_amdgcn_s_sleep(SW_SPIN_SLEEP);
+            auto flow_loop = [&](auto in_c, auto out_c) __attribute__((always_inline)) {
+                constexpr int IN = decltype(in_c)::value, OUT = decltype(out_c)::value;
+                constexpr int AIN = flow_aux(IN), AOUT = flow_aux(OUT);
+                // granule prefetch queue: gq[i] holds the loads for chunk c + i (issued SW_F2_GPREF chunks ahead)
+                u32x4 gq[SW_F2_GPREF];
+    #pragma unroll
+                for (int i = 0; i < SW_F2_GPREF; ++i)
+                    gq[i] = flow_granule(IN) ? fetch_granules<C, AIN>(in_e, i * C, lane, m) : u32x4{0u, 0u, 0u, 0u};
+                unsigned D[C / 4];
+                load_codes<C>(D, code_at(0));
+                int cons_seen = 0;
+                int h_avail = 0;                     // SW_F2_HALFLDS: the mid-chunk inflow read
+                int2 h_v = make_int2(0, 0);
+                int spec_avail = -1;                 // progress word read with spec_v (-1: none)
+                int2 spec_v = make_int2(0, 0);
+                // granule outflow at step k0 (chunk start, or mid-chunk with SW_F2_HALFPUB):
+                // lane L >= 64 - C holds row k0 - 128 + L; with half-chunk publishing only
+                // lanes >= 64 - C/2 are new
+                unsigned bp_seen = 0;   // ring mode: last value read of the consumer's progress word
+                auto publish_granules_half = [&](const int k0) __attribute__((always_inline)) {
+                    const int row_out = k0 - 128 + lane;
+                    constexpr int LO = SW_F2_HALFPUB ? 64 - C / 2 : 64 - C;
+                    const bool st = lane >= LO && row_out >= 0 && row_out < m;
+                    if (RING && bp_word != nullptr) {
+                        // rows <= k0 - 65 go out: positions <= pos0 + k0 - 65 - R must be consumed.
+                        // Also at the start of a round (k0 - 64 <= R): the slots then still hold the
+                        // previous round's last rows, which the consumer (one hop behind, in that
+                        // round) may not have read yet; `need` is then below pos0, in wrap-safe
+                        // unsigned arithmetic, and in round 0 below 0, so always met.
+                        const unsigned need = out_e.pos0 + (unsigned)(k0 - 64 - kp.ring_rows);
+                        if ((int)(bp_seen - need) < 0) {
                             bp_seen = __builtin_amdgcn_readfirstlane(
                                 __hip_atomic_load(bp_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-                            if ((long long)__builtin_amdgcn_s_memrealtime() - t_start > kp.timeout_ticks) {
-                                failed = true;
-                                if (fail_bp < 0) fail_bp = k0;
-                                break;
-                            }
-                        }
-                    }
-                }
-                edge_publish<AOUT>(out_e, row_out, st, IOH, LIN ? IOH : IOE);
-            };
-            // ---- publish the last chunk's outflow: lane L >= 64 - C holds row k0 - 128 + L
-            auto publish = [&](const int k0) __attribute__((always_inline)) {
-                const int row_out = k0 - 128 + lane;
-                if constexpr (OUT == FLOW_LDS) {
-                    // ring slots of rows < k0 - 64 - R must have been read
-                    const int floor_rows = k0 - 64 - R;
-                    if (cons_seen < floor_rows) {
-                        cons_seen = __builtin_amdgcn_readfirstlane(lds_load(&cons[wave + 1]));
-                        while (cons_seen < floor_rows) {
-                            __builtin_amdgcn_s_sleep(SW_SPIN_SLEEP);
-                            cons_seen = __builtin_amdgcn_readfirstlane(lds_load(&cons[wave + 1]));
-                            if ((long long)__builtin_amdgcn_s_memrealtime() - t_start > kp.timeout_ticks) {
-                                failed = true;
-                                break;
-                            }
-                        }
-                    }
-                    int2* const dst = lane >= 64 - HL ? &out_ring[row_out & (R - 1)] : &sink[wave][lane];
-                    *dst = make_int2(IOH, LIN ? IOH : IOE);
-                    compiler_fence();
-                    *prod_out = max(0, k0 - 64);   // after the ring writes (in-order DS)
-                } else if constexpr (flow_granule(OUT)) {
-                    publish_granules_half(k0);
-                }
-            };
-            for (int c = 0; c < nloc; ++c) {
-                const int k0 = c * C;
-#ifdef SW_TIMELINE
-                if (c == 1 || c == 2 || c == 3 || c == 50 || c == 1000)
-                    tl[c == 1 ? 0 : c == 2 ? 1 : c == 3 ? 2 : c == 50 ? 3 : 4] = realtime_waited();
-#endif
-                // ---- inflow rows [k0, k0 + C), for lanes [0, C) of the I/O registers
-                int newH, newE;
-                if constexpr (flow_granule(IN)) {
-                    u32x4 g = gq[0];
-                    if (kp.trace != nullptr) {   // tools: count chunks whose granules were not there yet
-                        const int row = k0 + lane;
-                        const bool need = lane < C && row < m;
-                        nslow += __all((!need) | granule_ok(g, in_e, row)) ? 0 : 1;
-                    }
-                    await_granules<C, AIN>(kp, in_e, g, k0, lane, m, strip, failed);
-                    if constexpr (RING) {
-                        if (kp.trace != nullptr && failed && fail_in < 0) fail_in = k0;
-                    }
-                    // ring mode: rows < k0 + C are consumed (reported every 4th chunk and at
-                    // the last).  An unconditional store, dropped (offset OOR) where there is
-                    // nothing to report: no branch around a memory op in the chunk loop.
-                    if constexpr (RING)
-                        __builtin_amdgcn_raw_buffer_store_b32(
-                            in_e.pos0 + (unsigned)min(k0 + C, m), cons_rsrc,
-                            cons_live && lane == 0 && ((c & 3) == 3 || c == nloc - 1) ? 0u : OOR, 0, AUX_SC1);
-#pragma unroll
-                    for (int i = 0; i + 1 < SW_F2_GPREF; ++i) gq[i] = gq[i + 1];
-                    if constexpr (SW_F2_GPOS == 0)
-                        gq[SW_F2_GPREF - 1] = fetch_granules<C, AIN>(in_e, k0 + SW_F2_GPREF * C, lane, m);
-                    const bool live = k0 + lane < m;
-                    newH = live ? (int)g.y : -go;
-                    newE = live ? (int)g.z : -ge;
-                } else if constexpr (IN == FLOW_LDS) {
-                    const int need = min(k0 + HL, m);
-                    int2 v;
-                    if constexpr (SW_F2_SPEC > 0) {
-                        // the rows were read speculatively during the last chunk, behind a read
-                        // of the progress word; only if that word did not cover them, poll and re-read
-                        v = spec_v;
-                        if (__builtin_amdgcn_readfirstlane(spec_avail) < need) {
-                            ++nslow;
-                            int avail = __builtin_amdgcn_readfirstlane(lds_load(&prod[in_w]));
-                            while (avail < need) {
+                            while ((int)(bp_seen - need) < 0) {
                                 __builtin_amdgcn_s_sleep(SW_SPIN_SLEEP);
-                                avail = __builtin_amdgcn_readfirstlane(lds_load(&prod[in_w]));
+                                bp_seen = __builtin_amdgcn_readfirstlane(
+                                    __hip_atomic_load(bp_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
                                 if ((long long)__builtin_amdgcn_s_memrealtime() - t_start > kp.timeout_ticks) {
                                     failed = true;
+                                    if (fail_bp < 0) fail_bp = k0;
                                     break;
                                 }
                             }
-                            compiler_fence();
-                            v = in_ring[(k0 + (lane & (C - 1))) & (R - 1)];
                         }
-                    } else {
-                        // the progress word and the chunk's rows in one LDS round trip (DS ops
-                        // of a wave execute in order: rows read after a word that covers them
-                        // are complete); re-read both until the word covers the chunk
-                        int avail = lds_load(&prod[in_w]);
+                    }
+                    edge_publish<AOUT>(out_e, row_out, st, IOH, LIN ? IOH : IOE);
+                };
+                // ---- publish the last chunk's outflow: lane L >= 64 - C holds row k0 - 128 + L
+                auto publish = [&](const int k0) __attribute__((always_inline)) {
+                    const int row_out = k0 - 128 + lane;
+                    if constexpr (OUT == FLOW_WRAP) {
+                        int2* const dst = lane >= 64 - HL && row_out >= 0 ? &wrapbuf[row_out] : &sink[wave][lane];
+                        *dst = make_int2(IOH, LIN ? IOH : IOE);
                         compiler_fence();
-                        v = in_ring[(k0 + (lane & (HL - 1))) & (R - 1)];
-                        if (__builtin_amdgcn_readfirstlane(avail) < need) {
-                            ++nslow;
-                            do {
+                        *prod_out = pb_out + max(0, k0 - 64);   // after the buffer writes (in-order DS)
+                    } else if constexpr (OUT == FLOW_LDS) {
+                        // ring slots of rows < k0 - 64 - R must have been read
+                        const int floor_rows = pb_out + k0 - 64 - R;
+                        int* const cons_next = &cons[(wave + 1) & 3];   // PWG wave 3: wave 0 of the next round
+                        if (cons_seen < floor_rows) {
+                            cons_seen = __builtin_amdgcn_readfirstlane(lds_load(cons_next));
+                            while (cons_seen < floor_rows) {
                                 __builtin_amdgcn_s_sleep(SW_SPIN_SLEEP);
-                                avail = lds_load(&prod[in_w]);
-                                compiler_fence();
-                                v = in_ring[(k0 + (lane & (HL - 1))) & (R - 1)];
+                                cons_seen = __builtin_amdgcn_readfirstlane(lds_load(cons_next));
                                 if ((long long)__builtin_amdgcn_s_memrealtime() - t_start > kp.timeout_ticks) {
                                     failed = true;
                                     break;
                                 }
-                            } while (__builtin_amdgcn_readfirstlane(avail) < need);
+                            }
                         }
+                        int2* const dst = lane >= 64 - HL ? &out_ring[(pb_out + row_out) & (R - 1)] : &sink[wave][lane];
+                        *dst = make_int2(IOH, LIN ? IOH : IOE);
+                        compiler_fence();
+                        *prod_out = pb_out + max(0, k0 - 64);   // after the ring writes (in-order DS)
+                    } else if constexpr (flow_granule(OUT)) {
+                        publish_granules_half(k0);
                     }
-                    newH = v.x;
-                    newE = v.y;
-                } else {
-                    newH = -go;
-                    newE = -ge;
-                }
-                // ---- scores of the chunk's rows: one v_perm_b32 per 4 rows
-                unsigned P[C / 4], PB[W2 ? C / 4 : 1];
-#pragma unroll
-                for (int u = 0; u < C / 4; ++u) P[u] = __builtin_amdgcn_perm(prof, 0x80808080u, D[u]);
-                if constexpr (W2) {
-#pragma unroll
-                    for (int u = 0; u < C / 4; ++u) PB[u] = __builtin_amdgcn_perm(profB, 0x80808080u, D[u]);
-                }
-                // take the inflow (and the scores) into registers before this chunk's LDS
-                // writes are issued, so the waits for them do not also wait for the writes
-                asm volatile("" : "+v"(newH), "+v"(newE));
-                if (c > 0) publish(k0);
-                IOH = newH;
-                IOE = newE;
-                if constexpr (IN == FLOW_LDS) {
-                    compiler_fence();
-                    *cons_out = k0 + HL;   // after the ring read (DS ops execute in order)
-                }
-#ifdef SW_TIMELINE
-                if (c == 0) t_first = realtime_waited();
-#endif
-                if constexpr (STREAM) {   // refill the ring: codes of chunk c+2, raw bytes of chunk c+3
-                    put_codes(rq0, c + 2);
-                    rq0 = raw_of(c + 3);
-                }
-                load_codes<C>(D, code_at(k0 + C));
-                // ---- C anti-diagonal steps
-#pragma unroll
-                for (int j = 0; j < C; j += 4) {
-                    if constexpr (flow_granule(IN) && SW_F2_GPOS > 0) {
-                        if (j == SW_F2_GPOS * C / 4) gq[SW_F2_GPREF - 1] = fetch_granules<C, AIN>(in_e, k0 + SW_F2_GPREF * C, lane, m);
-                    }
-                    if constexpr (flow_granule(OUT) && SW_F2_HALFPUB) {
-                        // lanes [64 - C/2, 64) hold this chunk's first C/2 outflow rows
-                        if (j == C / 2) publish_granules_half(k0 + C / 2);
-                    }
-                    if constexpr (OUT == FLOW_LDS && SW_F2_HALFLDS) {
-                        if (j == C / 2) publish(k0 + C / 2);
-                    }
-                    if constexpr (IN == FLOW_LDS && SW_F2_HALFLDS) {
-                        // the second half of the chunk's inflow: rows [k0 + C/2, k0 + C) go into
-                        // lanes [0, C/2) of the I/O registers just before step C/2, when lanes
-                        // [C/2, C) of the chunk start have rotated down there
-                        if (j == C / 2 - SW_F2_HALFIN_AHEAD) {
-                            h_avail = lds_load(&prod[in_w]);
-                            compiler_fence();
-                            h_v = in_ring[(k0 + HL + (lane & (HL - 1))) & (R - 1)];
+                };
+                for (int c = 0; c < nloc; ++c) {
+                    const int k0 = c * C;
+    #ifdef SW_TIMELINE
+                    if (c == 1 || c == 2 || c == 3 || c == 50 || c == 1000)
+                        tl[c == 1 ? 0 : c == 2 ? 1 : c == 3 ? 2 : c == 50 ? 3 : 4] = realtime_waited();
+    #endif
+                    // ---- inflow rows [k0, k0 + C), for lanes [0, C) of the I/O registers
+                    int newH, newE;
+                    if constexpr (flow_granule(IN)) {
+                        u32x4 g = gq[0];
+                        if (kp.trace != nullptr) {   // tools: count chunks whose granules were not there yet
+                            const int row = k0 + lane;
+                            const bool need = lane < C && row < m;
+                            nslow += __all((!need) | granule_ok(g, in_e, row)) ? 0 : 1;
                         }
-                        if (j == C / 2) {
-                            const int need = min(k0 + C, m);
-                            if (__builtin_amdgcn_readfirstlane(h_avail) < need) {
+                        await_granules<C, AIN>(kp, in_e, g, k0, lane, m, strip, failed);
+                        if constexpr (RING) {
+                            if (kp.trace != nullptr && failed && fail_in < 0) fail_in = k0;
+                        }
+                        // ring mode: rows < k0 + C are consumed (reported every 4th chunk and at
+                        // the last).  An unconditional store, dropped (offset OOR) where there is
+                        // nothing to report: no branch around a memory op in the chunk loop.
+                        if constexpr (RING)
+                            __builtin_amdgcn_raw_buffer_store_b32(
+                                in_e.pos0 + (unsigned)min(k0 + C, m), cons_rsrc,
+                                cons_live && lane == 0 && ((c & 3) == 3 || c == nloc - 1) ? 0u : OOR, 0, AUX_SC1);
+    #pragma unroll
+                        for (int i = 0; i + 1 < SW_F2_GPREF; ++i) gq[i] = gq[i + 1];
+                        if constexpr (SW_F2_GPOS == 0)
+                            gq[SW_F2_GPREF - 1] = fetch_granules<C, AIN>(in_e, k0 + SW_F2_GPREF * C, lane, m);
+                        const bool live = k0 + lane < m;
+                        newH = live ? (int)g.y : -go;
+                        newE = live ? (int)g.z : -ge;
+                    } else if constexpr (IN == FLOW_LDS || IN == FLOW_WRAP) {
+                        const int need = pb_in + min(k0 + HL, m);
+                        // the rows' slots: the producer's ring, or (WRAP) the round buffer
+                        auto in_slot = [&](const int row) __attribute__((always_inline)) -> const int2* {
+                            if constexpr (IN == FLOW_WRAP) return &wrapbuf[row];
+                            else return &in_ring[(pb_in + row) & (R - 1)];
+                        };
+                        int2 v;
+                        if constexpr (SW_F2_SPEC > 0) {
+                            // the rows were read speculatively during the last chunk, behind a read
+                            // of the progress word; only if that word did not cover them, poll and re-read
+                            v = spec_v;
+                            if (__builtin_amdgcn_readfirstlane(spec_avail) < need) {
                                 ++nslow;
-                                do {
+                                int avail = __builtin_amdgcn_readfirstlane(lds_load(&prod[in_w]));
+                                while (avail < need) {
                                     __builtin_amdgcn_s_sleep(SW_SPIN_SLEEP);
-                                    h_avail = lds_load(&prod[in_w]);
-                                    compiler_fence();
-                                    h_v = in_ring[(k0 + HL + (lane & (HL - 1))) & (R - 1)];
+                                    avail = __builtin_amdgcn_readfirstlane(lds_load(&prod[in_w]));
                                     if ((long long)__builtin_amdgcn_s_memrealtime() - t_start > kp.timeout_ticks) {
                                         failed = true;
                                         break;
                                     }
-                                } while (__builtin_amdgcn_readfirstlane(h_avail) < need);
+                                }
+                                compiler_fence();
+                                v = *in_slot(k0 + (lane & (C - 1)));
                             }
-                            IOH = lane < HL ? h_v.x : IOH;
-                            if constexpr (!LIN) IOE = lane < HL ? h_v.y : IOE;
-                            compiler_fence();
-                            *cons_out = k0 + C;   // after the ring read
-                        }
-                    }
-                    if constexpr (IN == FLOW_LDS && SW_F2_SPEC > 0) {
-                        if (j == C - SW_F2_SPEC) {   // speculative read of the next chunk's inflow
-                            spec_avail = lds_load(&prod[in_w]);
-                            compiler_fence();
-                            spec_v = in_ring[(k0 + C + (lane & (C - 1))) & (R - 1)];
-                            compiler_fence();
-                        }
-                    }
-                    auto step_lin = [&](auto b_c) __attribute__((always_inline)) {
-                        constexpr int b = decltype(b_c)::value;
-                        // 5.5 VALU: hgO = max(H - G, 0) in one clamped subtract carries the floor
-                        // at 0, so H = max(t, hgL, H_up - G, 0) = max3(hgL, hgO, t); hgL is a
-                        // tied DPP-add straight out of H, so the chain is H -> DPP-add -> max3
-                        // (C2 4.21 -> 3.64 ms, C5 285 -> 251 ms against H = max(max3(hgL, hgO, 0), t)
-                        // with hgO = H - G and hgL shifted out of hgO)
-                        const int t = L0 + sbyte<b>(P[j >> 2]);
-                        int ioh = L0;
-                        const int hgL = rot_dpp_add(IOH, ioh, H, neggo, hgO);
-                        IOH = ioh;
-                        H = vmax3(hgL, hgO, t);
-                        hgO = sub_clamp0(H, go);
-                        M = max(M, t);
-                        L0 = hgL;
-                    };
-                    auto step_lin2 = [&](auto b_c) __attribute__((always_inline)) {
-                        constexpr int b = decltype(b_c)::value;
-                        // 9 VALU for 128 cells.  Column A: as step_lin, with H_B of lane l-1 as
-                        // the left input.  Column B: diagonal = H_A of the last row taken
-                        // unshifted with the raw score byte (tB = H_A + s), left = max(H_A - G, 0)
-                        // of this row, which is hgO_A: the clamp only adds the 0 that
-                        // H = max(0, ...) has anyway, so no separate H_A - G is needed
-                        // The maxima stay inline asm (vmax3) although the compiler pads a read of an
-                        // asm result in the next instruction with s_nop 0 (it assumes a 16-bit dst_sel
-                        // write).  Compiler-visible maxima removed C2's 16-20 nops per 32 steps but the
-                        // kernel got slower (3.15 -> 3.30 ms: a lone wave's 4-step body times the same
-                        // either way, tools/ubench_w2seq.hip, and the rest of the chunk scheduled worse),
-                        // and the streamed kernels grew from 93 to 135 VGPRs (ring mode needs <= 128).
-                        const int tA = L0 + sbyte<b>(P[j >> 2]);
-                        const int tB = H + sbyte<b>(PB[j >> 2]);
-                        int ioh = L0;
-                        const int hgL = rot_dpp_add(IOH, ioh, HB, neggo, hgOB);   // HB -> hgOB -> DPP
-                        IOH = ioh;
-                        H = vmax3(hgL, hgO, tA);
-                        hgO = sub_clamp0(H, go);
-                        HB = vmax3(hgO, hgOB, tB);
-                        hgOB = sub_clamp0(HB, go);
-                        M = vmax3(M, tA, tB);
-                        L0 = hgL;
-                    };
-                    auto step = [&](auto b_c) __attribute__((always_inline)) {
-                        constexpr int b = decltype(b_c)::value;
-                        if constexpr (W2) {
-                            step_lin2(b_c);
-                        } else if constexpr (LIN) {
-                            step_lin(b_c);
                         } else {
+                            // the progress word and the chunk's rows in one LDS round trip (DS ops
+                            // of a wave execute in order: rows read after a word that covers them
+                            // are complete); re-read both until the word covers the chunk
+                            int avail = lds_load(&prod[in_w]);
+                            compiler_fence();
+                            v = *in_slot(k0 + (lane & (HL - 1)));
+                            if (__builtin_amdgcn_readfirstlane(avail) < need) {
+                                ++nslow;
+                                do {
+                                    __builtin_amdgcn_s_sleep(SW_SPIN_SLEEP);
+                                    avail = lds_load(&prod[in_w]);
+                                    compiler_fence();
+                                    v = *in_slot(k0 + (lane & (HL - 1)));
+                                    if ((long long)__builtin_amdgcn_s_memrealtime() - t_start > kp.timeout_ticks) {
+                                        failed = true;
+                                        break;
+                                    }
+                                } while (__builtin_amdgcn_readfirstlane(avail) < need);
+                            }
+                        }
+                        newH = v.x;
+                        newE = v.y;
+                        if constexpr (IN == FLOW_WRAP) {
+                            // rows >= m of the round buffer may hold anything (never written in
+                            // this pass): the border values instead, as for granule inflow
+                            const bool live = k0 + lane < m;
+                            newH = live ? newH : -go;
+                            newE = live ? newE : -ge;
+                        }
+                    } else {
+                        newH = -go;
+                        newE = -ge;
+                    }
+                    // ---- scores of the chunk's rows: one v_perm_b32 per 4 rows
+                    unsigned P[C / 4], PB[W2 ? C / 4 : 1];
+    #pragma unroll
+                    for (int u = 0; u < C / 4; ++u) P[u] = __builtin_amdgcn_perm(prof, 0x80808080u, D[u]);
+                    if constexpr (W2) {
+    #pragma unroll
+                        for (int u = 0; u < C / 4; ++u) PB[u] = __builtin_amdgcn_perm(profB, 0x80808080u, D[u]);
+                    }
+                    // take the inflow (and the scores) into registers before this chunk's LDS
+                    // writes are issued, so the waits for them do not also wait for the writes
+                    asm volatile("" : "+v"(newH), "+v"(newE));
+                    if (c > 0) publish(k0);
+                    IOH = newH;
+                    IOE = newE;
+                    if constexpr (IN == FLOW_LDS || IN == FLOW_WRAP) {
+                        compiler_fence();
+                        *cons_out = pb_in + k0 + HL;   // after the ring read (DS ops execute in order)
+                    }
+    #ifdef SW_TIMELINE
+                    if (c == 0) t_first = realtime_waited();
+    #endif
+                    if constexpr (STREAM) {   // refill the ring: codes of chunk c+2, raw bytes of chunk c+3
+                        put_codes(rq0, c + 2);
+                        rq0 = raw_of(c + 3);
+                    }
+                    load_codes<C>(D, code_at(k0 + C));
+                    // ---- C anti-diagonal steps
+    #pragma unroll
+                    for (int j = 0; j < C; j += 4) {
+                        if constexpr (flow_granule(IN) && SW_F2_GPOS > 0) {
+                            if (j == SW_F2_GPOS * C / 4) gq[SW_F2_GPREF - 1] = fetch_granules<C, AIN>(in_e, k0 + SW_F2_GPREF * C, lane, m);
+                        }
+                        if constexpr (flow_granule(OUT) && SW_F2_HALFPUB) {
+                            // lanes [64 - C/2, 64) hold this chunk's first C/2 outflow rows
+                            if (j == C / 2) publish_granules_half(k0 + C / 2);
+                        }
+                        if constexpr (OUT == FLOW_LDS && SW_F2_HALFLDS) {
+                            if (j == C / 2) publish(k0 + C / 2);
+                        }
+                        if constexpr (IN == FLOW_LDS && SW_F2_HALFLDS) {
+                            // the second half of the chunk's inflow: rows [k0 + C/2, k0 + C) go into
+                            // lanes [0, C/2) of the I/O registers just before step C/2, when lanes
+                            // [C/2, C) of the chunk start have rotated down there
+                            if (j == C / 2 - SW_F2_HALFIN_AHEAD) {
+                                h_avail = lds_load(&prod[in_w]);
+                                compiler_fence();
+                                h_v = in_ring[(pb_in + k0 + HL + (lane & (HL - 1))) & (R - 1)];
+                            }
+                            if (j == C / 2) {
+                                const int need = pb_in + min(k0 + C, m);
+                                if (__builtin_amdgcn_readfirstlane(h_avail) < need) {
+                                    ++nslow;
+                                    do {
+                                        __builtin_amdgcn_s_sleep(SW_SPIN_SLEEP);
+                                        h_avail = lds_load(&prod[in_w]);
+                                        compiler_fence();
+                                        h_v = in_ring[(pb_in + k0 + HL + (lane & (HL - 1))) & (R - 1)];
+                                        if ((long long)__builtin_amdgcn_s_memrealtime() - t_start > kp.timeout_ticks) {
+                                            failed = true;
+                                            break;
+                                        }
+                                    } while (__builtin_amdgcn_readfirstlane(h_avail) < need);
+                                }
+                                IOH = lane < HL ? h_v.x : IOH;
+                                if constexpr (!LIN) IOE = lane < HL ? h_v.y : IOE;
+                                compiler_fence();
+                                *cons_out = pb_in + k0 + C;   // after the ring read
+                            }
+                        }
+                        if constexpr (IN == FLOW_LDS && SW_F2_SPEC > 0) {
+                            if (j == C - SW_F2_SPEC) {   // speculative read of the next chunk's inflow
+                                spec_avail = lds_load(&prod[in_w]);
+                                compiler_fence();
+                                spec_v = in_ring[(pb_in + k0 + C + (lane & (C - 1))) & (R - 1)];
+                                compiler_fence();
+                            }
+                        }
+                        auto step_lin = [&](auto b_c) __attribute__((always_inline)) {
+                            constexpr int b = decltype(b_c)::value;
+                            // 5.5 VALU: hgO = max(H - G, 0) in one clamped subtract carries the floor
+                            // at 0, so H = max(t, hgL, H_up - G, 0) = max3(hgL, hgO, t); hgL is a
+                            // tied DPP-add straight out of H, so the chain is H -> DPP-add -> max3
+                            // (C2 4.21 -> 3.64 ms, C5 285 -> 251 ms against H = max(max3(hgL, hgO, 0), t)
+                            // with hgO = H - G and hgL shifted out of hgO)
                             const int t = L0 + sbyte<b>(P[j >> 2]);
-                            // rotate the I/O registers down one lane; lane 63 takes last step's
-                            // (hgL, ehL) = row k - 64 of the next strip's lane 0
-                            const int ioh = __builtin_amdgcn_update_dpp(L0, IOH, DPP_WAVE_SHL1, 0xF, 0xF, false);
-                            const int ioe = __builtin_amdgcn_update_dpp(ehP, IOE, DPP_WAVE_SHL1, 0xF, 0xF, false);
-                            const int F = max3i(fh, hgO, 0);
-                            const int hgL = dpp_add_shr1_tied(IOH, H, neggo, F);     // H -> hgO -> F -> DPP
-                            const int ehL = dpp_add_shr1_tied(IOE, E, negge, hgO);   // E -> H -> hgO -> DPP
+                            int ioh = L0;
+                            const int hgL = rot_dpp_add(IOH, ioh, H, neggo, hgO);
                             IOH = ioh;
-                            IOE = ioe;
-                            E = max3i(ehL, hgL, 0);
-                            fh = F - ge;
-                            H = vmax3(t, E, F);
-                            hgO = H - go;
+                            H = vmax3(hgL, hgO, t);
+                            hgO = sub_clamp0(H, go);
                             M = max(M, t);
                             L0 = hgL;
-                            ehP = ehL;
-                        }
-                    };
-                    step(std::integral_constant<int, 0>{});
-                    step(std::integral_constant<int, 1>{});
-                    step(std::integral_constant<int, 2>{});
-                    step(std::integral_constant<int, 3>{});
+                        };
+                        auto step_lin2 = [&](auto b_c) __attribute__((always_inline)) {
+                            constexpr int b = decltype(b_c)::value;
+                            // 9 VALU for 128 cells.  Column A: as step_lin, with H_B of lane l-1 as
+                            // the left input.  Column B: diagonal = H_A of the last row taken
+                            // unshifted with the raw score byte (tB = H_A + s), left = max(H_A - G, 0)
+                            // of this row, which is hgO_A: the clamp only adds the 0 that
+                            // H = max(0, ...) has anyway, so no separate H_A - G is needed
+                            // The maxima stay inline asm (vmax3) although the compiler pads a read of an
+                            // asm result in the next instruction with s_nop 0 (it assumes a 16-bit dst_sel
+                            // write).  Compiler-visible maxima removed C2's 16-20 nops per 32 steps but the
+                            // kernel got slower (3.15 -> 3.30 ms: a lone wave's 4-step body times the same
+                            // either way, tools/ubench_w2seq.hip, and the rest of the chunk scheduled worse),
+                            // and the streamed kernels grew from 93 to 135 VGPRs (ring mode needs <= 128).
+                            const int tA = L0 + sbyte<b>(P[j >> 2]);
+                            const int tB = H + sbyte<b>(PB[j >> 2]);
+                            int ioh = L0;
+                            const int hgL = rot_dpp_add(IOH, ioh, HB, neggo, hgOB);   // HB -> hgOB -> DPP
+                            IOH = ioh;
+                            H = vmax3(hgL, hgO, tA);
+                            hgO = sub_clamp0(H, go);
+                            HB = vmax3(hgO, hgOB, tB);
+                            hgOB = sub_clamp0(HB, go);
+                            M = vmax3(M, tA, tB);
+                            L0 = hgL;
+                        };
+                        auto step = [&](auto b_c) __attribute__((always_inline)) {
+                            constexpr int b = decltype(b_c)::value;
+                            if constexpr (W2) {
+                                step_lin2(b_c);
+                            } else if constexpr (LIN) {
+                                step_lin(b_c);
+                            } else {
+                                const int t = L0 + sbyte<b>(P[j >> 2]);
+                                // rotate the I/O registers down one lane; lane 63 takes last step's
+                                // (hgL, ehL) = row k - 64 of the next strip's lane 0
+                                const int ioh = __builtin_amdgcn_update_dpp(L0, IOH, DPP_WAVE_SHL1, 0xF, 0xF, false);
+                                const int ioe = __builtin_amdgcn_update_dpp(ehP, IOE, DPP_WAVE_SHL1, 0xF, 0xF, false);
+                                const int F = max3i(fh, hgO, 0);
+                                const int hgL = dpp_add_shr1_tied(IOH, H, neggo, F);     // H -> hgO -> F -> DPP
+                                const int ehL = dpp_add_shr1_tied(IOE, E, negge, hgO);   // E -> H -> hgO -> DPP
+                                IOH = ioh;
+                                IOE = ioe;
+                                E = max3i(ehL, hgL, 0);
+                                fh = F - ge;
+                                H = vmax3(t, E, F);
+                                hgO = H - go;
+                                M = max(M, t);
+                                L0 = hgL;
+                                ehP = ehL;
+                            }
+                        };
+                        step(std::integral_constant<int, 0>{});
+                        step(std::integral_constant<int, 1>{});
+                        step(std::integral_constant<int, 2>{});
+                        step(std::integral_constant<int, 3>{});
+                    }
                 }
+                publish(nloc * C);
+            };
+            dispatch_kinds<PWG ? KINDS_LDS : SLAB ? KINDS_PEER : KINDS_GRANULE>(in_kind, out_kind, flow_loop);
+            if (kp.trace != nullptr && lane == 0) {
+                unsigned long long* t = kp.trace + 16ull * (unsigned)strip;
+                t[0] = (unsigned long long)t_start;
+                t[1] = (unsigned long long)t_first;
+                t[3] = (unsigned long long)nslow;
+                t[13] = (unsigned long long)(long long)fail_in;
+                t[14] = (unsigned long long)(long long)fail_bp;
+                t[2] = (unsigned long long)__builtin_amdgcn_s_memrealtime();
+                t[7] = (unsigned long long)nloc;
+                for (int q = 0; q < 5; ++q) t[8 + q] = (unsigned long long)tl[q];
             }
-            publish(nloc * C);
-        };
-        dispatch_kinds<SLAB>(in_kind, out_kind, flow_loop);
-        if (kp.trace != nullptr && lane == 0) {
-            unsigned long long* t = kp.trace + 16ull * (unsigned)strip;
-            t[0] = (unsigned long long)t_start;
-            t[1] = (unsigned long long)t_first;
-            t[3] = (unsigned long long)nslow;
-            t[13] = (unsigned long long)(long long)fail_in;
-            t[14] = (unsigned long long)(long long)fail_bp;
-            t[2] = (unsigned long long)__builtin_amdgcn_s_memrealtime();
-            t[7] = (unsigned long long)nloc;
-            for (int q = 0; q < 5; ++q) t[8 + q] = (unsigned long long)tl[q];
+            if (failed && lane == 0) {
+                atomicOr(&kp.ctrl->error, ERR_TIMEOUT);
+                atomicMax(&kp.ctrl->err_item, (unsigned)strip);
+            }
+    #pragma unroll
+            for (int off = 32; off > 0; off >>= 1) M = max(M, __shfl_xor(M, off));
+            if (lane == 0 && M > 0) atomicMax(&kp.scores[pd.out_idx], M);
         }
-        if (failed && lane == 0) {
-            atomicOr(&kp.ctrl->error, ERR_TIMEOUT);
-            atomicMax(&kp.ctrl->err_item, (unsigned)strip);
-        }
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) M = max(M, __shfl_xor(M, off));
-        if (lane == 0 && M > 0) atomicMax(&kp.scores[pd.out_idx], M);
     }
 }
 
@@ -740,26 +784,29 @@ int flow2_dyn_lds(const LaunchCfg& cfg, int* lim) {
     const int wgs = STREAM ? std::max(1, std::min(cfg.f2_wgs, F2_WGS_MAX)) : 1;
     const int pad = LDS_PER_CU / (wgs + 1) + 1024 - flow2_static_lds(C, f2_loader<STREAM>() ? 5 : 4);
     *lim = flow2_stage_max(C) - (STREAM ? 4 * (F2_CR + C + 64) : 0);
+    if (STREAM && cfg.f2_pwg) return std::max(pad, 8 * flow2_pwg_rows(cfg.max_m, C));   // the round buffer
     return STREAM ? pad : std::max(flow2_stage_bytes(cfg.max_m, C), pad);
 }
 
-template <int C, bool STREAM, bool RING = false, bool SLAB = false, bool LIN = false, bool W2 = false>
+template <int C, bool STREAM, bool RING = false, bool SLAB = false, bool LIN = false, bool W2 = false,
+          bool PWG = false>
 hipError_t prepare_c(const LaunchCfg& cfg, int* dyn) {
     int lim = 0;
     *dyn = flow2_dyn_lds<C, STREAM>(cfg, &lim);
     if (*dyn > lim) return hipErrorInvalidValue;
     if (*dyn > 64 * 1024)   // raise the dynamic-LDS limit (once per variant and device)
-        return raise_dyn_lds((const void*)sw_flow2_kernel<C, STREAM, RING, SLAB, LIN, W2>, lim);
+        return raise_dyn_lds((const void*)sw_flow2_kernel<C, STREAM, RING, SLAB, LIN, W2, PWG>, lim);
     return hipSuccess;
 }
 
-template <int C, bool STREAM, bool RING = false, bool SLAB = false, bool LIN = false, bool W2 = false>
+template <int C, bool STREAM, bool RING = false, bool SLAB = false, bool LIN = false, bool W2 = false,
+          bool PWG = false>
 hipError_t launch_c(const LaunchCfg& cfg, const KParams& kp, hipStream_t s) {
     int dyn = 0;
-    const hipError_t e = prepare_c<C, STREAM, RING, SLAB, LIN, W2>(cfg, &dyn);
+    const hipError_t e = prepare_c<C, STREAM, RING, SLAB, LIN, W2, PWG>(cfg, &dyn);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL((sw_flow2_kernel<C, STREAM, RING, SLAB, LIN, W2>), dim3(cfg.blocks), dim3(f2_threads<STREAM>()),
-                       (size_t)dyn, s, kp);
+    hipLaunchKernelGGL((sw_flow2_kernel<C, STREAM, RING, SLAB, LIN, W2, PWG>), dim3(cfg.blocks),
+                       dim3(f2_threads<STREAM>()), (size_t)dyn, s, kp);
     return hipGetLastError();
 }
 
@@ -806,6 +853,14 @@ int waves_c() {
 bool flow2_variant_exists(int C) { return C == 16 || C == 32 || C == 64; }
 
 hipError_t launch_sw_flow2(const LaunchCfg& cfg, const KParams& kp, hipStream_t stream) {
+    // a pair per workgroup (batches needing int32 scores): 64-row chunks, throughput-bound,
+    // the two-column linear-gap step or the one-column affine step
+    if (cfg.f2_pwg) {
+        if (cfg.C != 64) return hipErrorInvalidValue;
+        return cfg.f2_w2 && cfg.f2_lin ? launch_c<64, true, false, false, true, true, true>(cfg, kp, stream)
+               : !cfg.f2_w2 && !cfg.f2_lin ? launch_c<64, true, false, false, false, false, true>(cfg, kp, stream)
+                                           : hipErrorInvalidValue;
+    }
     switch (cfg.C) {
         // the linear-gap step (G_INIT == G_EXT) is built for 32-row (latency-bound pairs) and
         // 64-row chunks (ring mode, throughput-bound)

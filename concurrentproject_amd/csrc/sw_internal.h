@@ -130,6 +130,7 @@ struct LaunchCfg {
     bool f2_lin = false;    // G_INIT == G_EXT, the exact linear-gap step: MODE_FLOW2 at C = 32 or 64 (sw_flow2.hip
                             // LIN) and MODE_DUO with duo_f16 (sw_kernels.hip StripDuo LIN)
     bool f2_w2 = false;     // MODE_FLOW2 with f2_lin: two columns per lane (126 new columns per strip)
+    bool f2_pwg = false;    // MODE_FLOW2 batch: a pair per workgroup, all hand-offs in LDS (C = 64, streamed)
 };
 constexpr int F2_WGS_MAX = 4;   // flow2 streamed kernel: most workgroups per CU (launch_c sizes the LDS pad)
 
@@ -158,6 +159,13 @@ __host__ __device__ constexpr int flow2_stage_bytes(int m, int C) {
 // (rings: 4, or 5 with the staged kernel's loader wave, whose static LDS bounds the staged rows)
 __host__ __device__ constexpr int flow2_static_lds(int C, int rings = 5) { return rings * (256 * 8 + 64 * 8 + 64 * 4) + 64 + 0 * C; }
 __host__ __device__ constexpr int flow2_stage_max(int C) { return LDS_PER_CU - flow2_static_lds(C) - 256; }
+// flow2 pair per workgroup (LaunchCfg::f2_pwg): the wave 3 -> wave 0 buffer holds a round's
+// rows (int2 each) in the dynamic LDS; workgroups per CU that fit beside the static LDS
+// (4 rings) and the 4 streamed code rings
+__host__ __device__ constexpr int flow2_pwg_rows(int m, int C) { return (m + 64 + C - 1) / C * C; }
+__host__ __device__ constexpr int flow2_pwg_wgs(int m, int C) {
+    return LDS_PER_CU / (8 * flow2_pwg_rows(m, C) + flow2_static_lds(C, 4) + 4 * (256 + C + 64) + 1024);
+}
 // sets the calling thread's sw_last_error() text (sw_engine.hip)
 void report_error(const char* msg);
 // hipFuncSetAttribute(fn, MaxDynamicSharedMemorySize, bytes) once per (kernel, device) (sw_engine.hip)

@@ -606,7 +606,7 @@ __global__ void __launch_bounds__(256) sw_flow_kernel(KParams kp) {
             }
             if (c < nloc) chunk(c, g0);
         };
-        dispatch_kinds<true>(in_kind, out_kind, flow_loop);
+        dispatch_kinds<KINDS_PEER>(in_kind, out_kind, flow_loop);
         if (kp.trace != nullptr && lane == 0) {
             unsigned long long* t = kp.trace + 16ull * (unsigned)strip;
             t[0] = (unsigned long long)t_start;

@@ -170,6 +170,9 @@ void sw_db_close(sw_db* db);
  *   "f2_wgs"   flow2 streamed kernel: workgroups per CU, 0 = auto, 1..4 (ring mode:
  *              lowered to what the runtime reports resident for its kernel)
  *   "f2stream" 1 = flow2 streams the row codes even when they fit in LDS (tests)
+ *   "f2pwg"    DNA batches whose scores need int32 (no 16-bit duos): -1 = (default) the
+ *              flow2 step with a pair per workgroup when its constants fit, 0 = never
+ *              (the pair-per-workgroup strip kernel), 1 = also for a forced mode 5 batch
  *   "trace"    device address of a 16 x u64 per-strip trace buffer, 0 = off (tools)
  * Returns 0, or -1 for an unknown key / bad value. */
 int sw_set_option(const char* key, long long value);
@@ -185,7 +188,7 @@ typedef struct {
     int mode;
     int variant;            /* bit 0: duo max3 via v_pk_maximum3_f16; bit 1: flow2 streams row codes;
                                bit 2: flow2 ring edges; bit 3: the linear-gap step;
-                               bit 4: flow2 two columns per lane */
+                               bit 4: flow2 two columns per lane; bit 5: flow2 pair per workgroup */
 } sw_stats;
 int sw_last_stats(sw_stats* out);
 

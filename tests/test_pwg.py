@@ -1,0 +1,111 @@
+"""GPU parity: the flow2 kernel with a pair per workgroup (sw_flow2.hip PWG, option
+f2pwg), the path of DNA batches whose scores need int32, against the oracle,
+bit-exact.  Every hand-off of a pair goes through its workgroup's LDS rings, wave 3
+to wave 0 of the next round included; the shapes cut the strips into rounds of 1-4
+strips, rows around the 64-row chunk, both steps (two columns per lane with the
+linear-gap step, one column with the affine step), grids smaller than the batch."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ACGT = np.frombuffer(b"ACGT", np.uint8)
+OPTS = ("W", "C", "blocks", "orient", "f2stream", "f2_wgs")
+
+
+def _rand_dna(rng, n):
+    return ACGT[rng.integers(0, 4, n)]
+
+
+def _pairs(rng, shapes):
+    out = []
+    for n, m in shapes:
+        a = _rand_dna(rng, n)
+        b = _rand_dna(rng, m)
+        if rng.random() < 0.5 and m > 10:
+            b = np.resize(a, m).copy()        # long diagonals through every strip and round edge
+            mut = rng.random(m) < 0.05
+            b[mut] = _rand_dna(rng, int(mut.sum()))
+        out.append((a, b))
+    return out
+
+
+@pytest.fixture(autouse=True)
+def _defaults(engine):
+    def reset():
+        engine.set_params(engine.Params())
+        for k in OPTS:
+            engine.set_option(k, 0)
+        engine.set_option("mode", -1)
+        engine.set_option("linear", -1)
+        engine.set_option("f2w", 0)
+        engine.set_option("f2pwg", -1)
+    reset()
+    yield
+    reset()
+
+
+# strips at two columns per lane: 1 (n <= 128), 2, 4, 5, 8, 9, 16 ...; rows below, at and
+# around the 64-row chunk
+SHAPES = [(1, 1), (5, 200), (128, 64), (129, 63), (254, 65), (255, 129), (504, 1000), (505, 127), (630, 700),
+          (1009, 1), (1010, 2000), (1135, 333), (2017, 2100), (3000, 4097), (4096, 999), (8000, 8192)]
+
+
+def test_pwg_forced_matches_oracle(engine, oracle_mod):
+    """f2pwg = 1 with mode 5: ragged batch, linear-gap and affine constants, the
+    automatic grid and grids of 1 and 3 workgroups (each runs many pairs)."""
+    rng = np.random.default_rng(21)
+    pairs = _pairs(rng, SHAPES)
+    engine.set_option("orient", 1)
+    engine.set_option("mode", 5)
+    engine.set_option("f2pwg", 1)
+    for prm in (engine.Params(), engine.Params(2, -3, 5, 2), engine.Params(3, -2, 4, 4), engine.Params(1, 0, 0, 0)):
+        op = oracle_mod.Params(prm.match, prm.mismatch, prm.gap_init, prm.gap_ext)
+        exp = [oracle_mod.score_linear(a, b, op) for a, b in pairs]
+        for blocks in (0, 1, 3):
+            engine.set_option("blocks", blocks)
+            assert engine.score_batch(pairs, prm) == exp, (prm, blocks)
+            st = engine.last_stats()
+            lin = prm.gap_init == prm.gap_ext
+            assert st["mode"] == 5 and st["variant"] & 32 and st["C"] == 64, st
+            assert bool(st["variant"] & 16) == lin and bool(st["variant"] & 8) == lin, st
+            assert st["items"] == len(pairs) and st["boundary_bytes"] == 0, st
+
+
+def test_pwg_is_the_int32_batch_path(engine, oracle_mod):
+    """A DNA batch whose scores may reach 2^16 (MATCH * min(n, m) + MATCH > 65535) takes
+    PWG automatically; f2pwg = 0 falls back to the pair-per-workgroup strip kernel."""
+    rng = np.random.default_rng(22)
+    pairs = _pairs(rng, [(700, 700), (690, 710), (705, 650), (800, 720), (701, 702), (650, 800)])
+    prm = engine.Params(100, -20, 20, 20)        # 100 * 650 + 100 > 65535: no 16-bit duos
+    op = oracle_mod.Params(100, -20, 20, 20)
+    exp = [oracle_mod.score_linear(a, b, op) for a, b in pairs]
+    assert max(exp) > 30000
+    assert engine.score_batch(pairs, prm) == exp
+    st = engine.last_stats()
+    assert st["mode"] == 5 and st["variant"] & 32, st
+    engine.set_option("f2pwg", 0)
+    assert engine.score_batch(pairs, prm) == exp
+    assert engine.last_stats()["mode"] != 5
+
+
+def test_pwg_config_c3_on_int32(engine, golden):
+    """The C3 batch (1024 pairs N = 8192, seeds 8192+k) on the int32 PWG kernel against
+    its golden.  Its scores fit 16 bits, so the duo kernel would take it; the int32 path
+    is forced (mode 5, f2pwg 1)."""
+    import torch
+    c = golden("configs.json")["C3"]
+    N, P, exp = c["N"], c["npairs"], c["scores"]
+    host = engine.gen_batch(c["seed_base"], P, N)
+    arena = torch.from_numpy(host).cuda()
+    scores = torch.full((P,), -1, dtype=torch.int32, device="cuda")
+    s = torch.cuda.current_stream()
+    engine.set_option("mode", 5)
+    engine.set_option("f2pwg", 1)
+    engine.score_batch_device(arena.data_ptr(), [2 * N * k for k in range(P)], [N] * P,
+                              [2 * N * k + N for k in range(P)], [N] * P, scores.data_ptr(), flags=1,
+                              stream=s.cuda_stream)
+    engine.stream_status(s.cuda_stream)
+    st = engine.last_stats()
+    assert st["mode"] == 5 and st["variant"] & 32 and st["variant"] & 16, st
+    assert scores.cpu().tolist() == exp[:P]

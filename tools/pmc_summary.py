@@ -20,6 +20,12 @@ For each workload (c2 -> pair, c3 -> batch, c5 -> slab on one GPU):
         reads), WRITE_SIZE is exact for the 16-B/lane granule stores; the
         1-B/lane row reads are uncalibrated (< 1 % of the total).
     Every counter group came from its own --pmc pass with nothing traced.
+  * adds valu_mix: the fast / slow instruction-class fractions of the kernel's
+    chunk loop (tools/issue_model.py, from a -save-temps compile of the same
+    sources), which bench.py prices with the measured issue costs
+    (profiles/r03_ubench_issue_classes.jsonl) for roofline.issue.
+
+    python tools/pmc_summary.py --mix-only     # add / refresh valu_mix of the existing pmc_*.json
 """
 import csv
 import hashlib
@@ -67,7 +73,45 @@ def sha256(path):
     return h.hexdigest()
 
 
+def valu_mix(kernel):
+    """issue_model.kernel_mix of `kernel` (demangled name) from build/asm/<src>.s, compiled
+    with the library's flags when missing or older than its source."""
+    import subprocess
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import issue_model
+    csrc = os.path.join(ROOT, "concurrentproject_amd", "csrc")
+    base = "sw_flow2" if "sw_flow2_kernel" in kernel else "sw_kernels"
+    out = os.path.join(ROOT, "build", "asm")
+    s_path = os.path.join(out, base + "-hip-amdgcn-amd-amdhsa-gfx950.s")
+    deps = [os.path.join(csrc, f) for f in (base + ".hip", "sw_device.h", "sw_internal.h")]
+    if not os.path.exists(s_path) or os.path.getmtime(s_path) < max(os.path.getmtime(d) for d in deps):
+        os.makedirs(out, exist_ok=True)
+        subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-c",
+                        "-save-temps", os.path.join(csrc, base + ".hip"), "-o", os.path.join(out, base + ".o")],
+                       cwd=out, check=True, stderr=subprocess.DEVNULL)
+    km = issue_model.kernel_mix(s_path, issue_model.mangled_filter(kernel))
+    if km is None:
+        return None
+    km["source_sha256"] = source_stamp()
+    km["method"] = "static census of the kernel's chunk loop (tools/issue_model.py kernel_mix)"
+    return km
+
+
+def mix_only():
+    for wl in WORKLOAD.values():
+        path = os.path.join(ROOT, "profiles", "pmc_%s.json" % wl)
+        if not os.path.exists(path):
+            continue
+        out = json.load(open(path))
+        out["valu_mix"] = valu_mix(out["kernel"])
+        with open(path, "w") as f:
+            json.dump(out, f, indent=1)
+        print(wl, json.dumps(out["valu_mix"]))
+
+
 def main():
+    if sys.argv[1] == "--mix-only":
+        return mix_only()
     src, rnd = sys.argv[1], sys.argv[2]
     prof = os.path.join(ROOT, "profiles")
     for cfg in ("c2", "c3", "c5"):
@@ -122,6 +166,7 @@ def main():
             out["GRBM_GUI_ACTIVE"] = g
             out["clock_ghz"] = g / 8 / t_ns
             passes.append("GRBM_GUI_ACTIVE")
+        out["valu_mix"] = valu_mix(k)
         out["method"] = ("rocprofv3 --pmc, one pass per group, nothing else traced: " + "; ".join(passes) +
                          "; kernel time from the --kernel-trace --stats run of the same command")
         with open(os.path.join(prof, "pmc_%s.json" % WORKLOAD[cfg]), "w") as f:

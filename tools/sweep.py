@@ -71,17 +71,22 @@ def run_case(sw, torch, spec, reps):
     return {"case": spec, "mode": st["mode"], "W": st["W"], "C": st["C"], "items": st["items"], "blocks": st["blocks"],
             "ms_med": round(med, 4), "ms_min": round(ms[0], 4), "gcups": round(cells / med / 1e6, 2),
             "ns_per_strip_step": round(med * 1e6 / steps, 2) if n <= 64 * st["W"] else None,
-            "score0": int(scores[0].item())}
+            "score0": int(scores[0].item()), "scores_sum": int(scores.sum().item()),
+            "variant": st["variant"], "waves_per_cu": st["waves_per_cu"]}
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--cases", default=DEFAULT)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--opt", action="append", default=[], help="engine option k=v (sw_set_option), repeatable")
     args = ap.parse_args()
     import torch
     import concurrentproject_amd as sw
     torch.cuda.set_device(0)
+    for kv in args.opt:
+        k, v = kv.split("=")
+        sw.set_option(k, int(v))
     for spec in args.cases.split(","):
         t0 = time.time()
         try:
