@@ -131,16 +131,23 @@ def test_slab_edges_are_system_scope():
     with tempfile.TemporaryDirectory() as d:
         for text in codeobj.disassemble(lib, d):
             funcs.update(codeobj.functions(text))
-    pat = re.compile(r"sw_flow2_kernelILi(\d+)ELb(\d)ELb(\d)ELb(\d)ELb(\d)E")
+    # <C, STREAM, RING, SLAB, LIN[, W2[, PWG]]>
+    pat = re.compile(r"sw_flow2_kernelILi(\d+)ELb(\d)ELb(\d)ELb(\d)ELb(\d)E(?:Lb(\d)E)?(?:Lb(\d)E)?")
     seen = {0: 0, 1: 0}
+    pwg = 0
     for name, body in funcs.items():
         m = pat.search(name)
         if not m:
             continue
         slab = int(m.group(4))
-        seen[slab] += 1
         g_loads = [x for x in body if x.startswith("buffer_load_dwordx4")]
         g_stores = [x for x in body if x.startswith("buffer_store_dwordx4")]
+        if m.group(7) == "1":
+            # a pair per workgroup: every hand-off in LDS, no granule at all
+            assert not g_loads and not g_stores, name
+            pwg += 1
+            continue
+        seen[slab] += 1
         assert g_loads and g_stores, name
         sys_ops = [x for x in g_loads + g_stores if "sc0 sc1" in x]
         if slab:
@@ -150,4 +157,4 @@ def test_slab_edges_are_system_scope():
         else:
             assert not sys_ops, (name, sys_ops[:3])
             assert all(" sc1" in x for x in g_stores), name
-    assert seen[0] >= 6 and seen[1] >= 3, seen
+    assert seen[0] >= 6 and seen[1] >= 3 and pwg >= 2, (seen, pwg)
