@@ -237,6 +237,14 @@ def roofline(workload, per_launch_cells, avg_kern_ms, step_ns=None, n=0, m=0, w2
         out["step_ns"] = round(step_ns, 3)
         out["wavefront_steps"] = m + 63 * strips
         out["critical_path_frac"] = round((m + 63 * strips) * step_ns / (avg_kern_ms * 1e6), 4)
+        # the same path at the lone-wave issue time of the bare two-column step body (no
+        # hand-offs, no chunk work: tools/ubench_w2seq.hip, 4 steps of the compiled W2 loop)
+        body = os.path.join(ROOT, "profiles", "r03_ubench_w2_step_body.jsonl")
+        if w2 and os.path.exists(body):
+            rows = [json.loads(l) for l in open(body) if l.startswith("{")]
+            body_ns = min(r["ns_per_4steps"] for r in rows) / 4
+            out["step_body_ns"] = round(body_ns, 3)
+            out["issue_path_frac"] = round((m + 63 * strips) * body_ns / (avg_kern_ms * 1e6), 4)
     return out
 
 
