@@ -383,10 +383,10 @@ void plan_flow2(Job& job, bool w2, bool pwg = false) {
 
 // The pair-per-workgroup kernel keeps a round's rows of its longest pair in LDS: at least
 // `wgs` such workgroups must fit a CU (automatic choice: 2, m up to ~8.5k rows).
-bool pwg_fits(const Job& job, int wgs) {
+bool pwg_fits(const Job& job, const Params& prm, int wgs) {
     int max_m = 0;
     for (const PairDesc& d : job.pairs) max_m = std::max(max_m, d.m);
-    return flow2_pwg_wgs(max_m, 64) >= wgs;
+    return flow2_pwg_wgs(max_m, 64, flow2_w2_wanted(job, prm)) >= wgs;
 }
 
 // A batch on the pair-per-workgroup flow2 kernel: W = 1 strips, 64-row chunks, streamed
@@ -414,7 +414,7 @@ int finalize_mode(Job& job, const Params& prm) {
     if (job.mode == MODE_FLOW2 && job.pairs.size() > 1 && g_opt_f2pwg.load() == 1) {
         Job w1 = job;   // a forced flow2 batch, a pair per workgroup (W = 1 strips, C = 64)
         plan(w1, 1, 64, false, MODE_FLOW2);
-        if (flow2_fits(w1, prm) && pwg_fits(w1, 1)) {
+        if (flow2_fits(w1, prm) && pwg_fits(w1, prm, 1)) {
             job = w1;
             plan_pwg(job, prm);
             return 0;
@@ -466,7 +466,7 @@ int finalize_mode(Job& job, const Params& prm) {
         if (g_opt_f2pwg.load() != 0 && job.pairs.size() > 1 && job.dna) {
             Job w1 = job;
             plan(w1, 1, 64, false, MODE_CHAIN);
-            if (flow2_fits(w1, prm) && pwg_fits(w1, 2)) {
+            if (flow2_fits(w1, prm) && pwg_fits(w1, prm, 2)) {
                 job = w1;
                 plan_pwg(job, prm);
             }
@@ -585,14 +585,16 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
         const int per_cu = job.item_base[np] / c->cus;
         f2_wgs = o > 0           ? (int)o
                  : job.ring      ? std::min(F2_WGS_MAX, std::max(1, per_cu / 2))
-                 : job.pwg       ? std::min({F2_WGS_MAX, std::max(1, per_cu), flow2_pwg_wgs(max_m_all, job.C)})
+                 : job.pwg       ? std::min({F2_WGS_MAX, std::max(1, per_cu), flow2_pwg_wgs(max_m_all, job.C, job.f2w2)})
                  : per_cu >= 4   ? 2
                                  : 1;
     }
-    // G_INIT == G_EXT: the exact linear-gap step (sw_flow2.hip LIN), unless disabled
-    const bool f2_lin = ((job.mode == MODE_FLOW2 && (job.C == 32 || job.C == 64)) ||
-                         (job.mode == MODE_DUO && job.duo_f16)) &&
-                        prm.gap_init == prm.gap_ext && g_opt_linear.load() != 0;
+    // G_INIT == G_EXT: the exact linear-gap step (sw_flow2.hip LIN), unless disabled; the
+    // pair-per-workgroup kernel is built with it exactly at two columns per lane
+    const bool f2_lin = job.pwg ? job.f2w2
+                                : ((job.mode == MODE_FLOW2 && (job.C == 32 || job.C == 64)) ||
+                                   (job.mode == MODE_DUO && job.duo_f16)) &&
+                                      prm.gap_init == prm.gap_ext && g_opt_linear.load() != 0;
     // read once: it sizes the ring arena here and addresses it in the kernel (kp.ring_rows)
     const long long ring_rows = g_opt_ring_rows.load();
     int ring_blocks = 0, wrap_rows = 0;

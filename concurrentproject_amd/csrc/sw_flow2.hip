@@ -356,7 +356,8 @@ __global__ void __launch_bounds__(f2_threads<STREAM>()) sw_flow2_kernel(KParams 
             // of round k - 1 stay until wave 0 of round k has read them: wave 3 writes row x
             // of round k only after wave 0 of round k has computed row x, so it needs no
             // back-pressure, which would close a cycle of waits 0 -> 1 -> 2 -> 3 -> 0)
-            int2* const wrapbuf = reinterpret_cast<int2*>(rc);
+            int2* const wrapbuf = reinterpret_cast<int2*>(rc);   // affine: (H - G_INIT, E - G_EXT)
+            int* const wrapbuf1 = reinterpret_cast<int*>(rc);    // LIN: H - G
             const Edge in_e = group_edge(kp, pd, group - 1, ngroups);
             const Edge out_e = group_edge(kp, pd, group, ngroups);
             // ring mode: the consumer of ring j reports the positions it has consumed in
@@ -479,8 +480,14 @@ __global__ void __launch_bounds__(f2_threads<STREAM>()) sw_flow2_kernel(KParams 
                 auto publish = [&](const int k0) __attribute__((always_inline)) {
                     const int row_out = k0 - 128 + lane;
                     if constexpr (OUT == FLOW_WRAP) {
-                        int2* const dst = lane >= 64 - HL && row_out >= 0 ? &wrapbuf[row_out] : &sink[wave][lane];
-                        *dst = make_int2(IOH, LIN ? IOH : IOE);
+                        const bool st = lane >= 64 - HL && row_out >= 0;
+                        if constexpr (LIN) {   // (H - G, H - G): one int per row
+                            int* const dst = st ? &wrapbuf1[row_out] : &psink[wave][lane];
+                            *dst = IOH;
+                        } else {
+                            int2* const dst = st ? &wrapbuf[row_out] : &sink[wave][lane];
+                            *dst = make_int2(IOH, IOE);
+                        }
                         compiler_fence();
                         *prod_out = pb_out + max(0, k0 - 64);   // after the buffer writes (in-order DS)
                     } else if constexpr (OUT == FLOW_LDS) {
@@ -542,9 +549,15 @@ __global__ void __launch_bounds__(f2_threads<STREAM>()) sw_flow2_kernel(KParams 
                     } else if constexpr (IN == FLOW_LDS || IN == FLOW_WRAP) {
                         const int need = pb_in + min(k0 + HL, m);
                         // the rows' slots: the producer's ring, or (WRAP) the round buffer
-                        auto in_slot = [&](const int row) __attribute__((always_inline)) -> const int2* {
-                            if constexpr (IN == FLOW_WRAP) return &wrapbuf[row];
-                            else return &in_ring[(pb_in + row) & (R - 1)];
+                        auto in_slot = [&](const int row) __attribute__((always_inline)) -> int2 {
+                            if constexpr (IN == FLOW_WRAP && LIN) {
+                                const int h = wrapbuf1[row];
+                                return make_int2(h, h);
+                            } else if constexpr (IN == FLOW_WRAP) {
+                                return wrapbuf[row];
+                            } else {
+                                return in_ring[(pb_in + row) & (R - 1)];
+                            }
                         };
                         int2 v;
                         if constexpr (SW_F2_SPEC > 0) {
@@ -563,7 +576,7 @@ __global__ void __launch_bounds__(f2_threads<STREAM>()) sw_flow2_kernel(KParams 
                                     }
                                 }
                                 compiler_fence();
-                                v = *in_slot(k0 + (lane & (C - 1)));
+                                v = in_slot(k0 + (lane & (C - 1)));
                             }
                         } else {
                             // the progress word and the chunk's rows in one LDS round trip (DS ops
@@ -571,14 +584,14 @@ __global__ void __launch_bounds__(f2_threads<STREAM>()) sw_flow2_kernel(KParams 
                             // are complete); re-read both until the word covers the chunk
                             int avail = lds_load(&prod[in_w]);
                             compiler_fence();
-                            v = *in_slot(k0 + (lane & (HL - 1)));
+                            v = in_slot(k0 + (lane & (HL - 1)));
                             if (__builtin_amdgcn_readfirstlane(avail) < need) {
                                 ++nslow;
                                 do {
                                     __builtin_amdgcn_s_sleep(SW_SPIN_SLEEP);
                                     avail = lds_load(&prod[in_w]);
                                     compiler_fence();
-                                    v = *in_slot(k0 + (lane & (HL - 1)));
+                                    v = in_slot(k0 + (lane & (HL - 1)));
                                     if ((long long)__builtin_amdgcn_s_memrealtime() - t_start > kp.timeout_ticks) {
                                         failed = true;
                                         break;
@@ -784,7 +797,8 @@ int flow2_dyn_lds(const LaunchCfg& cfg, int* lim) {
     const int wgs = STREAM ? std::max(1, std::min(cfg.f2_wgs, F2_WGS_MAX)) : 1;
     const int pad = LDS_PER_CU / (wgs + 1) + 1024 - flow2_static_lds(C, f2_loader<STREAM>() ? 5 : 4);
     *lim = flow2_stage_max(C) - (STREAM ? 4 * (F2_CR + C + 64) : 0);
-    if (STREAM && cfg.f2_pwg) return std::max(pad, 8 * flow2_pwg_rows(cfg.max_m, C));   // the round buffer
+    if (STREAM && cfg.f2_pwg)   // the round buffer
+        return std::max(pad, flow2_pwg_row_bytes(cfg.f2_lin) * flow2_pwg_rows(cfg.max_m, C));
     return STREAM ? pad : std::max(flow2_stage_bytes(cfg.max_m, C), pad);
 }
 

@@ -162,9 +162,12 @@ __host__ __device__ constexpr int flow2_stage_max(int C) { return LDS_PER_CU - f
 // flow2 pair per workgroup (LaunchCfg::f2_pwg): the wave 3 -> wave 0 buffer holds a round's
 // rows (int2 each) in the dynamic LDS; workgroups per CU that fit beside the static LDS
 // (4 rings) and the 4 streamed code rings
+// (4 B per row at the linear-gap step, whose edges carry H - G twice)
 __host__ __device__ constexpr int flow2_pwg_rows(int m, int C) { return (m + 64 + C - 1) / C * C; }
-__host__ __device__ constexpr int flow2_pwg_wgs(int m, int C) {
-    return LDS_PER_CU / (8 * flow2_pwg_rows(m, C) + flow2_static_lds(C, 4) + 4 * (256 + C + 64) + 1024);
+__host__ __device__ constexpr int flow2_pwg_row_bytes(bool lin) { return lin ? 4 : 8; }
+__host__ __device__ constexpr int flow2_pwg_wgs(int m, int C, bool lin) {
+    return LDS_PER_CU /
+           (flow2_pwg_row_bytes(lin) * flow2_pwg_rows(m, C) + flow2_static_lds(C, 4) + 4 * (256 + C + 64) + 1024);
 }
 // sets the calling thread's sw_last_error() text (sw_engine.hip)
 void report_error(const char* msg);

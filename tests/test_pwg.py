@@ -70,6 +70,14 @@ def test_pwg_forced_matches_oracle(engine, oracle_mod):
             assert st["mode"] == 5 and st["variant"] & 32 and st["C"] == 64, st
             assert bool(st["variant"] & 16) == lin and bool(st["variant"] & 8) == lin, st
             assert st["items"] == len(pairs) and st["boundary_bytes"] == 0, st
+        # one column per lane at the linear-gap constants (f2w = 1): the affine PWG step
+        if prm.gap_init == prm.gap_ext:
+            engine.set_option("f2w", 1)
+            engine.set_option("blocks", 2)
+            assert engine.score_batch(pairs, prm) == exp, (prm, "f2w=1")
+            st = engine.last_stats()
+            assert st["variant"] & 32 and not st["variant"] & 24, st
+            engine.set_option("f2w", 0)
 
 
 def test_pwg_is_the_int32_batch_path(engine, oracle_mod):
