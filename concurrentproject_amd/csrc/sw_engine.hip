@@ -578,13 +578,15 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
     //   N = 2^18 (1040)         32.4 25.2 26.2 26.4 | 31.7 26.3 34.2 32.1
     //   N = 2^19 (2080)         116 83.9 80.1 78.9  | 117 83.2 88.5 96.2
     //   N = 2^20 (4162, C5)     437 312 287 283     | 454 307 299 -
-    // ring: one per 2 CUs' worth of groups, up to 4; linear edges: 2 from 4 groups per CU
+    // ring: one per 2 CUs' worth of groups, up to 4, or one round of all groups when they fit
+    // (below); linear edges: 2 from 4 groups per CU
     int f2_wgs = 1;
     if (f2s) {
         const long long o = g_opt_f2_wgs.load();
         const int per_cu = job.item_base[np] / c->cus;
         f2_wgs = o > 0           ? (int)o
-                 : job.ring      ? std::min(F2_WGS_MAX, std::max(1, per_cu / 2))
+                 : job.ring      ? (job.item_base[np] <= c->cus * F2_WGS_MAX ? F2_WGS_MAX
+                                                                             : std::min(F2_WGS_MAX, std::max(1, per_cu / 2)))
                  : job.pwg       ? std::min({F2_WGS_MAX, std::max(1, per_cu), flow2_pwg_wgs(max_m_all, job.C, job.f2w2)})
                  : per_cu >= 4   ? 2
                                  : 1;
@@ -616,7 +618,19 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
             set_err("flow2 ring mode: the runtime reports %d resident workgroups per CU for its kernel", fit);
             return -1;
         }
-        ring_blocks = std::min(job.item_base[np], c->cus * f2_wgs);
+        const int items_all = job.item_base[np];
+        ring_blocks = std::min(items_all, c->cus * f2_wgs);
+        if (g_opt_f2_wgs.load() <= 0 && items_all <= c->cus * f2_wgs) {
+            // every group in one round (one block each) when they fit the resident blocks:
+            // a second round of a few groups runs them alone on their SIMDs after the rest.
+            // Measured (column slab 0 alone): 1/8 of C5, 260 groups: 256 blocks (2 rounds)
+            // 51.7 ms -> 260 blocks 42.7 ms; 1/4, 520 groups: 512 blocks 77.8 -> 520 60.8 ms.
+            // More groups than that keep one block per 2 CUs' worth of groups, a multiple of
+            // the CU count (the dispatcher then loads every CU evenly: C5's 2081 groups on
+            // 1024 blocks 181.8 ms, on 1041 blocks at up to 5 per CU 205.7 ms).
+            ring_blocks = items_all;
+            f2_wgs = std::max(1, (items_all + c->cus - 1) / c->cus);
+        }
         if (g_opt_blocks.load() > 0) ring_blocks = (int)std::min<long long>(g_opt_blocks.load(), job.item_base[np]);
         if (ring_blocks > c->cus * fit) {
             set_err("flow2 ring mode needs all %d workgroups co-resident (%d fit per CU, %d CUs)", ring_blocks, fit,
@@ -1207,8 +1221,8 @@ int sw_set_option(const char* key, long long v) {
         g_opt_duo_f16 = v ? 1 : 0;
     } else if (k == "f2stream") {   // 1 = flow2 streams row codes even when they fit in LDS (tests)
         g_opt_f2stream = v ? 1 : 0;
-    } else if (k == "f2_wgs") {   // flow2 streamed kernel: workgroups per CU, 0 = auto, 1..4
-        if (v < 0 || v > 4) return -1;
+    } else if (k == "f2_wgs") {   // flow2 streamed kernel: workgroups per CU, 0 = auto, 1..F2_WGS_MAX
+        if (v < 0 || v > F2_WGS_MAX) return -1;
         g_opt_f2_wgs = v;
     } else if (k == "f2w") {   // flow2 columns per lane: 0 auto, 1, 2 (2: the linear-gap step only)
         if (v < 0 || v > 2) return -1;
