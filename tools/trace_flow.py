@@ -51,6 +51,8 @@ def main():
     sw.set_option("trace", 0)
     sw.stream_status(s.cuda_stream)
     t = trace.cpu().numpy().reshape(strips, 16).astype(np.int64)
+    if os.environ.get("TRACE_DUMP"):   # the raw per-strip records (s_memrealtime, 100 MHz)
+        np.save(os.environ["TRACE_DUMP"], t)
     t0 = t[:, 0].min()
     start, first, end, spins = (t[:, 0] - t0) * 10, (t[:, 1] - t0) * 10, (t[:, 2] - t0) * 10, t[:, 3]   # ns
     lag = np.diff(first)
