@@ -94,6 +94,15 @@ __device__ __forceinline__ int rot_dpp_add(int io, int& rot, int src, int k, int
         : "+v"(old), "+v"(rot) : "v"(src), "v"(k), "v"(after));
     return old;
 }
+#ifndef SW_F2_VISMAX
+#define SW_F2_VISMAX 0      // 1: the staged W2 step's maxima compiler-visible (no asm-result nops; see step_lin2)
+#endif
+// max3: compiler-visible (VIS) or the inline-asm v_max3_i32 (sw_device.h vmax3)
+template <bool VIS>
+__device__ __forceinline__ int max3_sel(int a, int b, int c) {
+    if constexpr (VIS) return max(max(a, b), c);
+    else return vmax3(a, b, c);
+}
 // max(H - G, 0) for H >= 0 in one instruction (unsigned subtract, clamped at 0)
 __device__ __forceinline__ int sub_clamp0(int h, int g) {
     return (int)__builtin_elementwise_sub_sat((unsigned)h, (unsigned)g);
@@ -197,7 +206,7 @@ __global__ void __launch_bounds__(f2_threads<STREAM>()) sw_flow2_kernel(KParams 
     static_assert(!(RING || SLAB) || STREAM, "ring and slab kernels stream the row codes");
     static_assert(!W2 || LIN, "two columns per lane: the linear-gap step only");
     static_assert(!PWG || (STREAM && !RING && !SLAB), "pair per workgroup: streamed codes, LDS links only");
-    static_assert(!PWG || (SW_F2_SPEC == 0 && !SW_F2_HALFLDS), "pair per workgroup: whole-chunk LDS reads");
+    static_assert(!PWG || !SW_F2_HALFLDS, "pair per workgroup: whole-chunk LDS reads");
     static_assert(C % 4 == 0 && 64 % C == 0 && 2 * C + 64 <= F2_R, "chunk");
     // STREAM ring: during chunk c the reads span rows [k0 + C - 63, k0 + 2C) and the
     // writes rows [k0 + 2C, k0 + 3C): no slot is rewritten while still read
@@ -560,7 +569,7 @@ __global__ void __launch_bounds__(f2_threads<STREAM>()) sw_flow2_kernel(KParams 
                             }
                         };
                         int2 v;
-                        if constexpr (SW_F2_SPEC > 0) {
+                        if constexpr (SW_F2_SPEC > 0 && IN == FLOW_LDS) {
                             // the rows were read speculatively during the last chunk, behind a read
                             // of the progress word; only if that word did not cover them, poll and re-read
                             v = spec_v;
@@ -723,11 +732,11 @@ __global__ void __launch_bounds__(f2_threads<STREAM>()) sw_flow2_kernel(KParams 
                             int ioh = L0;
                             const int hgL = rot_dpp_add(IOH, ioh, HB, neggo, hgOB);   // HB -> hgOB -> DPP
                             IOH = ioh;
-                            H = vmax3(hgL, hgO, tA);
+                            H = max3_sel<SW_F2_VISMAX && !STREAM>(hgL, hgO, tA);
                             hgO = sub_clamp0(H, go);
-                            HB = vmax3(hgO, hgOB, tB);
+                            HB = max3_sel<SW_F2_VISMAX && !STREAM>(hgO, hgOB, tB);
                             hgOB = sub_clamp0(HB, go);
-                            M = vmax3(M, tA, tB);
+                            M = max3_sel<SW_F2_VISMAX && !STREAM>(M, tA, tB);
                             L0 = hgL;
                         };
                         auto step = [&](auto b_c) __attribute__((always_inline)) {
