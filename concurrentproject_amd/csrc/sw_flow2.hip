@@ -94,6 +94,9 @@ __device__ __forceinline__ int rot_dpp_add(int io, int& rot, int src, int k, int
         : "+v"(old), "+v"(rot) : "v"(src), "v"(k), "v"(after));
     return old;
 }
+#ifndef SW_F2_PRIO
+#define SW_F2_PRIO 0        // staged kernel: s_setprio of the compute waves (the loader stays at 0)
+#endif
 #ifndef SW_F2_VISMAX
 #define SW_F2_VISMAX 0      // 1: the staged W2 step's maxima compiler-visible (no asm-result nops; see step_lin2)
 #endif
@@ -341,6 +344,7 @@ __global__ void __launch_bounds__(f2_threads<STREAM>()) sw_flow2_kernel(KParams 
         for (int round = 0; round < nrounds; ++round) {
             const int strip = PWG ? 4 * round + wave : 4 * group + wave;
             if (strip >= pd.strips) break;
+            if constexpr (LD && SW_F2_PRIO > 0) __builtin_amdgcn_s_setprio(SW_F2_PRIO);   // ahead of the loader on SIMD 0
             const int pb_out = PWG ? round * span + 128 : 0;                       // positions this strip publishes at
             const int pb_in = PWG ? (wave > 0 ? round : round - 1) * span + 128 : 0;   // and reads at
             const int col = W2 ? 126 * strip + 2 * lane : 63 * strip + lane;
