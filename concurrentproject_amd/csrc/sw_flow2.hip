@@ -2,9 +2,14 @@
 // N = 65536) for gfx950.  Same recurrence and clamped arithmetic as
 // sw_kernels.hip (main.cpp:54-66, DESIGN.md "Arithmetic"); what changes is how
 // few instructions one anti-diagonal step costs.  For one long pair the time is
-// (m + strips x lag) steps of ONE wave per SIMD issuing alone (~4 cycles per
-// instruction, 2-4x more for LDS stores: MI355X_MICROARCH.md, LDS), so every
-// instruction of the step is on the critical path.
+// (m + strips x lag) steps of ONE wave per SIMD issuing alone (one VALU instruction
+// every ~2.05 ns, ~1.7 ns more per s_nop or SALU between two of them:
+// tools/ubench_bank.hip), so every instruction of the step is on the critical path.
+// The kernels that run many strips per SIMD (streamed, ring, slab, PWG) are bound
+// by VALU issue instead (roofline.issue).
+//
+// The affine one-column step is described here; the linear-gap step (LIN) and the
+// two-columns-per-lane step (W2, the automatic choice at G_INIT == G_EXT) below.
 //
 // Layout: a wave owns a strip of 64 columns, lane l = column 63*s + l.  Strips
 // OVERLAP by one column: lane 0 of strip s+1 recomputes column 63*(s+1), the
@@ -30,8 +35,9 @@
 // Hand-offs: wave w -> w+1 of a workgroup through an LDS ring with progress
 // words (as sw_flow_kernel); the workgroup edges through tagged HBM granules
 // (sw_device.h).  Work items (groups of 4 strips) are claimed in order, so a
-// producer is always resident: no co-residency assumption, any grid size.
-// Every spin is bounded by s_memrealtime and reports ERR_TIMEOUT.
+// producer is always resident: no co-residency assumption, any grid size (ring
+// mode deals them statically instead, every block resident; PWG claims whole
+// pairs).  Every spin is bounded by s_memrealtime and reports ERR_TIMEOUT.
 #include <algorithm>
 #include <type_traits>
 

@@ -907,8 +907,10 @@ __device__ void strip_pass_duo(const KParams& kp, const DuoDesc& d, const int st
 
 // Kernel 4 (DNA batches, 16-bit scores): workgroup b scores duos b, b+gridDim,
 // ...; its DUO_WAVES waves run strips w, w+DUO_WAVES, ... of each duo (as
-// sw_pairwg_kernel).  Four waves: eight (four per SIMD at C3) measured 3% slower
-// (12.43 vs 12.06 ms), so the step is issue-bound, not latency-bound.
+// sw_pairwg_kernel).  Four waves: eight (four per SIMD at C3) measured slower
+// (r01 12.43 vs 12.06 ms; r03 7.57 vs 7.44 ms): the step is issue-bound, and its
+// slow-class instructions (v_pk_*, v_perm, DPP) cost the SIMD ~1.8 ns at 2 waves
+// and at 4 alike (tools/ubench_bank.hip).
 // M3: H = max3 and the running max fold two positions per v_pk_maximum3_f16
 // (scores below 0x7C00 only, LaunchCfg::duo_f16).
 template <int W, int C, bool M3, bool LIN>
