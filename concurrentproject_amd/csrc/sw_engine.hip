@@ -399,7 +399,16 @@ void plan_pwg(Job& job, const Params& prm) {
     job.f2_stream = true;
 }
 
-int finalize_mode(Job& job, const Params& prm) {
+// A DNA batch on the flow2 item claim: a pair's strip groups spread over many CUs (W = 1
+// strips, 64-row chunks, streamed codes, 2 workgroups per CU from 4 groups per CU).
+void plan_claim(Job& job, const Params& prm) {
+    job.W = 1;
+    job.C = 64;
+    plan_flow2(job, flow2_w2_wanted(job, prm));
+    job.f2_stream = true;
+}
+
+int finalize_mode(Job& job, const Params& prm, int cus) {
     int max_m = 0;
     for (const PairDesc& d : job.pairs) max_m = std::max(max_m, d.m);
     // a single pair too wide for W = 1 under the 2048-strip rule: flow2 still runs it
@@ -451,6 +460,29 @@ int finalize_mode(Job& job, const Params& prm) {
     }
     const bool forced_duo = job.mode == MODE_DUO;
     if (forced_duo || (g_opt_mode.load() < 0 && job.mode == MODE_PAIRWG)) {
+        // DNA batches by size (measured, DESIGN.md section 8, kernel ms for duo / PWG / item claim):
+        //   fewer pairs than CUs: the flow2 item claim spreads each pair's strip groups
+        //     (128 x 8192: 3.87 / 3.53 / 2.46; 128 x 16384: 14.2 / 12.1 / 8.9; 16 x 65536: pairwg
+        //     316 / - / 17-18);
+        //   fewer than 2 per CU: a pair per workgroup (256 x 8192: 3.92 / 3.24 / 4.68;
+        //     256 x 4096: 1.27 / 0.96 / 1.38);
+        //   more: the 16-bit duos when exact (512 x 8192: 4.02 / 5.40 / 8.83; C3: 7.29 / 9.95 /
+        //     15.1), else a pair per workgroup, else the item claim.
+        const int P = (int)job.pairs.size();
+        const bool flow2_auto = !forced_duo && P > 1 && job.dna && g_opt_f2pwg.load() != 0;
+        Job w1 = job;
+        if (flow2_auto) plan(w1, 1, 64, false, MODE_CHAIN);
+        const bool f2ok = flow2_auto && flow2_fits(w1, prm);
+        if (f2ok && P < cus) {
+            job = w1;
+            plan_claim(job, prm);
+            return 0;
+        }
+        if (f2ok && P < 2 * cus && pwg_fits(w1, prm, 2)) {
+            job = w1;
+            plan_pwg(job, prm);
+            return 0;
+        }
         if (duo_fits(job, prm)) {
             job.mode = MODE_DUO;
             job.duo_f16 = duo_f16_fits(job, prm);
@@ -461,15 +493,12 @@ int finalize_mode(Job& job, const Params& prm) {
             set_err("duo mode needs an {A,C,G,T} batch whose scores fit 16 bits (MATCH*min(n,m)+MATCH <= 65535)");
             return -1;
         }
-        // scores that need int32: the flow2 step with a pair per workgroup when it applies
-        // (C3-shaped batch on int32: pairwg 18.9 ms -> flow2 PWG, sw_flow2.hip)
-        if (g_opt_f2pwg.load() != 0 && job.pairs.size() > 1 && job.dna) {
-            Job w1 = job;
-            plan(w1, 1, 64, false, MODE_CHAIN);
-            if (flow2_fits(w1, prm) && pwg_fits(w1, prm, 2)) {
-                job = w1;
-                plan_pwg(job, prm);
-            }
+        // scores that need int32: the flow2 step with a pair per workgroup when its round
+        // buffer fits (C3-shaped batch on int32: pairwg 18.8 ms -> PWG 9.95 ms), else the item claim
+        if (f2ok) {
+            job = w1;
+            if (pwg_fits(w1, prm, 2)) plan_pwg(job, prm);
+            else plan_claim(job, prm);
         }
     }
     return 0;
@@ -493,7 +522,7 @@ int plan_slab(Job& job, int n, int m, bool dna, const Params& prm) {
     const int W = fw ? (int)fw : 1;
     const long long fm = g_opt_mode.load();
     plan(job, W, pick_C(W), true, fm >= 0 ? (int)fm : MODE_CHAIN);
-    if (finalize_mode(job, prm)) return -1;
+    if (finalize_mode(job, prm, 256)) return -1;   // one pair: the CU count plays no part
     if (!grouped_mode(job.mode)) {
         set_err("a column slab needs a grouped kernel (chain, flow or flow2), not mode %d", job.mode);
         return -1;
@@ -845,7 +874,7 @@ int score_host(const HostPair* in, int npairs, const Params& prm, int* out) {
     }
     const int W = pick_W(job.pairs, single);
     plan(job, W, pick_C(W), single);
-    if (finalize_mode(job, prm)) return -1;
+    if (finalize_mode(job, prm, c->cus)) return -1;
     if (c->seq.ensure(bytes, s) || c->scores.ensure(act.size(), s) || c->hscores.ensure(act.size())) return -1;
     HIPCHK(hipMemcpyAsync(c->seq.p, c->hseq.p, bytes, hipMemcpyHostToDevice, s));
     if (enqueue(c, job, prm, c->seq.p, c->scores.p, (int)act.size(), s, true)) return -1;
@@ -1041,7 +1070,7 @@ int sw_score_batch_device(const unsigned char* d_arena, const int64_t* a_off, co
         HIPCHK(hipStreamSynchronize(s));
         job.dna = *hflag == 0;
     }
-    if (finalize_mode(job, prm)) return -1;
+    if (finalize_mode(job, prm, c->cus)) return -1;
     if (enqueue(c, job, prm, d_arena, d_scores, npairs, s, !stream)) return -1;
     if (!stream) {
         if (check_ctrl(c, s)) return -1;

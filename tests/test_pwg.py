@@ -81,20 +81,46 @@ def test_pwg_forced_matches_oracle(engine, oracle_mod):
 
 
 def test_pwg_is_the_int32_batch_path(engine, oracle_mod):
-    """A DNA batch whose scores may reach 2^16 (MATCH * min(n, m) + MATCH > 65535) takes
-    PWG automatically; f2pwg = 0 falls back to the pair-per-workgroup strip kernel."""
+    """A DNA batch whose scores may reach 2^16 (MATCH * min(n, m) + MATCH > 65535), as
+    many pairs as CUs or more, takes PWG automatically; fewer pairs than CUs take the
+    flow2 item claim; f2pwg = 0 falls back to the pair-per-workgroup strip kernel."""
+    import torch
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
     rng = np.random.default_rng(22)
-    pairs = _pairs(rng, [(700, 700), (690, 710), (705, 650), (800, 720), (701, 702), (650, 800)])
-    prm = engine.Params(100, -20, 20, 20)        # 100 * 650 + 100 > 65535: no 16-bit duos
+    shapes = [(int(rng.integers(680, 720)), int(rng.integers(680, 720))) for _ in range(cus + 40)]
+    pairs = _pairs(rng, shapes)
+    prm = engine.Params(100, -20, 20, 20)        # 100 * 680 + 100 > 65535: no 16-bit duos
     op = oracle_mod.Params(100, -20, 20, 20)
     exp = [oracle_mod.score_linear(a, b, op) for a, b in pairs]
     assert max(exp) > 30000
     assert engine.score_batch(pairs, prm) == exp
     st = engine.last_stats()
     assert st["mode"] == 5 and st["variant"] & 32, st
+    assert engine.score_batch(pairs[:6], prm) == exp[:6]
+    st = engine.last_stats()
+    assert st["mode"] == 5 and not st["variant"] & 32 and st["variant"] & 2, st   # item claim, streamed
     engine.set_option("f2pwg", 0)
-    assert engine.score_batch(pairs, prm) == exp
+    assert engine.score_batch(pairs[:40], prm) == exp[:40]
     assert engine.last_stats()["mode"] != 5
+
+
+def test_batch_kernel_by_batch_size(engine, oracle_mod):
+    """Automatic choice for DNA batches that fit 16 bits: fewer pairs than CUs -> the
+    flow2 item claim, fewer than 2 per CU -> a pair per workgroup, more -> duos; the
+    same scores every way."""
+    import torch
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    rng = np.random.default_rng(23)
+    shapes = [(int(rng.integers(560, 640)), int(rng.integers(560, 640))) for _ in range(2 * cus + 16)]
+    pairs = _pairs(rng, shapes)
+    exp = [oracle_mod.score_linear(a, b) for a, b in pairs]
+    for count, mode, pwg in ((cus // 2, 5, False), (cus + 16, 5, True), (2 * cus + 16, 3, False)):
+        assert engine.score_batch(pairs[:count]) == exp[:count], count
+        st = engine.last_stats()
+        assert st["mode"] == mode and bool(st["variant"] & 32) == pwg, (count, st)
+    engine.set_option("mode", 3)   # the duo kernel forced on the smallest batch
+    assert engine.score_batch(pairs[:cus // 2]) == exp[:cus // 2]
+    assert engine.last_stats()["mode"] == 3
 
 
 def test_pwg_config_c3_on_int32(engine, golden):
