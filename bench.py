@@ -536,7 +536,7 @@ def main():
                      "kernel_gcups": round(bcells / (bk * 1e-3) / 1e9, 3),
                      "parity": ("ok" if bsc == ref[:len(bsc)] else "MISMATCH")
                      if defaults and len(ref) >= len(bsc) == 1024 * world else "unchecked",
-                     "kernel": {3: "duo", 1: "pairwg"}.get(bst["mode"], bst["mode"]),
+                     "kernel": {3: "duo", 1: "pairwg", 5: "flow2"}.get(bst["mode"], bst["mode"]),
                      "dtype": "u16x2 (packed, exact: scores < 2^16)" if bst["mode"] == 3 else "int32",
                      "roofline": roofline("batch", bcells, bk, waves_per_simd=resident_waves_per_simd(bst, torch))}
         if extra is not None and world == 1:
