@@ -825,6 +825,9 @@ struct StripDuo {
     __device__ __forceinline__ void run(const u16x2 go2, const u16x2 ge2, const u16x2 ma2, const u16x2 gom2) {
         constexpr int U = W < 2 ? 2 : W;
         static_assert(C % U == 0, "a chunk is a whole number of slot rotations");
+#ifdef SW_DUO_UNROLL
+#pragma unroll SW_DUO_UNROLL
+#endif
         for (int s = 0; s < C; s += U) steps<0, U>(go2, ge2, ma2, gom2);
     }
 
