@@ -826,7 +826,9 @@ struct StripDuo {
         constexpr int U = W < 2 ? 2 : W;
         static_assert(C % U == 0, "a chunk is a whole number of slot rotations");
 #ifdef SW_DUO_UNROLL
-#pragma unroll SW_DUO_UNROLL
+#define SW_PRAGMA_(x) _Pragma(#x)
+#define SW_PRAGMA(x) SW_PRAGMA_(x)
+        SW_PRAGMA(unroll SW_DUO_UNROLL)
 #endif
         for (int s = 0; s < C; s += U) steps<0, U>(go2, ge2, ma2, gom2);
     }
