@@ -686,6 +686,16 @@ __device__ __forceinline__ DuoDesc load_duo(const KParams& kp, int idx) {
 // LIN (G_INIT == G_EXT, the reference's defaults): E+ = sat(H_left - G) and
 // F+ = sat(H_up - G) exactly (sw_flow2.hip, LIN), so a position keeps A and hg
 // only: 5.5 VALU per position and 5 per step instead of 9.5 and 7.
+// The chunk's steps unrolled whole by default: the rolled loop's back edge made the
+// compiler copy 8 row-code / A registers per iteration and keep the chunk's loop
+// overhead (C3, W = 8: 7.26 -> 7.06 ms; W = 4: 8.11 -> 7.74 ms at 8 of 16 iterations,
+// profiles/r03_ab/duo_unroll.txt).
+#ifndef SW_DUO_UNROLL
+#define SW_DUO_UNROLL 64
+#endif
+#define SW_PRAGMA_(x) _Pragma(#x)
+#define SW_PRAGMA(x) SW_PRAGMA_(x)
+
 template <int W, bool M3, bool LIN = false>
 struct StripDuo {
     unsigned pA[W], pB[W];                   // column penalty words: pair 0 (perm src1), pair 1 (perm src0)
@@ -825,11 +835,7 @@ struct StripDuo {
     __device__ __forceinline__ void run(const u16x2 go2, const u16x2 ge2, const u16x2 ma2, const u16x2 gom2) {
         constexpr int U = W < 2 ? 2 : W;
         static_assert(C % U == 0, "a chunk is a whole number of slot rotations");
-#ifdef SW_DUO_UNROLL
-#define SW_PRAGMA_(x) _Pragma(#x)
-#define SW_PRAGMA(x) SW_PRAGMA_(x)
         SW_PRAGMA(unroll SW_DUO_UNROLL)
-#endif
         for (int s = 0; s < C; s += U) steps<0, U>(go2, ge2, ma2, gom2);
     }
 
