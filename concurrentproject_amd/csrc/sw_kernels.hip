@@ -56,6 +56,12 @@ namespace {
 // ---------------------------------------------------------------------------
 // Per-lane state of one strip pass (W columns per lane).
 // ---------------------------------------------------------------------------
+#define SW_PRAGMA_(x) _Pragma(#x)
+#define SW_PRAGMA(x) SW_PRAGMA_(x)
+#ifndef SW_STRIP_UNROLL
+#define SW_STRIP_UNROLL 2   // step pairs per rolled iteration of the int32 strip chunk
+#endif
+
 template <int W, bool DNA>
 struct Strip {
     int prof[W], tb[W];                     // column profile / bias (fixed for the strip)
@@ -137,7 +143,7 @@ struct Strip {
 
     template <int C>
     __device__ __forceinline__ void run(const bool l63, const int go, const int ge, const int ma, const int mi) {
-#pragma unroll 2
+        SW_PRAGMA(unroll SW_STRIP_UNROLL)
         for (int s = 0; s < C; s += 2) {
             step(hgA, hgB, l63, go, ge, ma, mi);
             step(hgB, hgA, l63, go, ge, ma, mi);
@@ -693,8 +699,6 @@ __device__ __forceinline__ DuoDesc load_duo(const KParams& kp, int idx) {
 #ifndef SW_DUO_UNROLL
 #define SW_DUO_UNROLL 64
 #endif
-#define SW_PRAGMA_(x) _Pragma(#x)
-#define SW_PRAGMA(x) SW_PRAGMA_(x)
 
 template <int W, bool M3, bool LIN = false>
 struct StripDuo {
