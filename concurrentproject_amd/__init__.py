@@ -73,7 +73,7 @@ def source_stamp() -> str:
     h = hashlib.sha256()
     csrc = os.path.join(HERE, "csrc")
     files = sorted(glob.glob(os.path.join(csrc, "*.hip")) + glob.glob(os.path.join(csrc, "*.h")) +
-                   glob.glob(os.path.join(csrc, "*.cpp")) +
+                   glob.glob(os.path.join(csrc, "*.cpp")) + glob.glob(os.path.join(csrc, "*.inc")) +
                    [os.path.join(csrc, "Makefile"), os.path.join(HERE, "..", "include", "algoGPU.h")])
     for f in files:
         h.update(os.path.basename(f).encode())

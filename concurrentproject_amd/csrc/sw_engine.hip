@@ -58,7 +58,7 @@ Params g_params;
 
 std::atomic<long long> g_opt_W{0}, g_opt_C{0}, g_opt_bytes{0}, g_opt_timeout{30}, g_opt_blocks{0}, g_opt_orient{0},
     g_opt_mode{-1}, g_opt_trace{0}, g_opt_duo_f16{1}, g_opt_f2stream{0}, g_opt_ring{-1}, g_opt_ring_rows{4096}, g_opt_f2_wgs{0}, g_opt_f2w{0}, g_opt_f2pwg{-1},
-    g_opt_linear{-1};
+    g_opt_linear{-1}, g_opt_f3{1};
 
 // Longest sequence the engine takes: granule buffers of m rows keep m * 16 in the
 // 32-bit record count of a buffer resource (sw_device.h linear_edge).
@@ -700,6 +700,10 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
     cfg.f2_lin = f2_lin;
     cfg.f2_w2 = job.mode == MODE_FLOW2 && job.f2w2;
     cfg.f2_pwg = job.mode == MODE_FLOW2 && job.pwg;
+    // the staged two-column linear-gap kernel with hand-scheduled chunk loops (sw_flow3.hip), unless
+    // option f3 = 0: C2
+    cfg.f3 = g_opt_f3.load() != 0 && cfg.f2_w2 && f2_lin && !f2s && !cfg.f2_pwg && !job.ring && job.C == 32 &&
+             flow3_fits(max_m);
     if (cfg.f2_w2 && !f2_lin) {   // the strips were cut for two columns per lane
         set_err("flow2: two columns per lane needs the linear-gap step");
         return -1;
@@ -731,7 +735,10 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
     kp.scores = d_scores;
     kp.npairs = (int)np;
     kp.total_items = items;
-    if (++c->epoch == 0) ++c->epoch;
+    // epochs are never 0 (tag of a zeroed granule), nor the one that makes flow3's granule
+    // key epoch ^ 0x5BD1E995 zero (a zeroed 8-B granule would then pass its check)
+    do ++c->epoch;
+    while (c->epoch == 0 || c->epoch == 0x5BD1E995u);
     kp.epoch = c->epoch;
     kp.match = prm.match;
     kp.mismatch = prm.mismatch;
@@ -767,7 +774,8 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
     }
 
     if (time_kernel) HIPCHK(hipEventRecord(c->ev0, s));
-    HIPCHK(job.mode == MODE_FLOW2 ? launch_sw_flow2(cfg, kp, s) : launch_sw_strip(cfg, kp, s));
+    HIPCHK(cfg.f3 ? launch_sw_flow3(cfg, kp, s)
+           : job.mode == MODE_FLOW2 ? launch_sw_flow2(cfg, kp, s) : launch_sw_strip(cfg, kp, s));
     if (time_kernel) HIPCHK(hipEventRecord(c->ev1, s));
 
     t_stats = sw_stats{};
@@ -780,7 +788,7 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
     t_stats.items = items;
     t_stats.mode = job.mode;
     t_stats.variant = (cfg.duo_f16 ? 1 : 0) | (cfg.f2_stream ? 2 : 0) | (job.ring ? 4 : 0) | (cfg.f2_lin ? 8 : 0) |
-                      (cfg.f2_w2 ? 16 : 0) | (cfg.f2_pwg ? 32 : 0);
+                      (cfg.f2_w2 ? 16 : 0) | (cfg.f2_pwg ? 32 : 0) | (cfg.f3 ? 64 : 0);
     t_stats.boundary_bytes = (long long)(job.bnd_granules * sizeof(Granule));
     c->last = s;
     return 0;
@@ -1262,6 +1270,9 @@ int sw_set_option(const char* key, long long v) {
     } else if (k == "linear") {   // G_INIT == G_EXT: -1 auto (the linear-gap step), 0 = the affine step
         if (v < -1 || v > 0) return -1;
         g_opt_linear = v;
+    } else if (k == "f3") {   // 1 (default): staged W2 linear-gap launches on flow3 (sw_flow3.hip), 0: flow2
+        if (v < 0 || v > 1) return -1;
+        g_opt_f3 = v;
     } else if (k == "ring") {   // flow2 one-pair group edges: -1 auto (rings above 1 GB of edges), 0 off, 1 on
         if (v < -1 || v > 1) return -1;
         g_opt_ring = v;
@@ -1294,6 +1305,7 @@ long long sw_get_option(const char* key) {
     if (k == "ring_rows") return g_opt_ring_rows;
     if (k == "f2w") return g_opt_f2w;
     if (k == "f2pwg") return g_opt_f2pwg;
+    if (k == "f3") return g_opt_f3;
     return -1;
 }
 

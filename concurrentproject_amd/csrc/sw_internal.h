@@ -131,6 +131,7 @@ struct LaunchCfg {
                             // LIN) and MODE_DUO with duo_f16 (sw_kernels.hip StripDuo LIN)
     bool f2_w2 = false;     // MODE_FLOW2 with f2_lin: two columns per lane (126 new columns per strip)
     bool f2_pwg = false;    // MODE_FLOW2 batch: a pair per workgroup, all hand-offs in LDS (C = 64, streamed)
+    bool f3 = false;        // MODE_FLOW2 staged two-column linear-gap launch on the flow3 kernel (sw_flow3.hip)
 };
 constexpr int F2_WGS_MAX = 4;   // flow2 streamed kernel: most workgroups per CU (launch_c sizes the LDS pad)
 
@@ -175,6 +176,9 @@ void report_error(const char* msg);
 hipError_t raise_dyn_lds(const void* fn, int bytes);
 
 hipError_t launch_sw_flow2(const LaunchCfg& cfg, const KParams& kp, hipStream_t stream);
+// flow3 (sw_flow3.hip): flow2's staged W2 linear-gap kernel with hand-scheduled chunk loops
+hipError_t launch_sw_flow3(const LaunchCfg& cfg, const KParams& kp, hipStream_t stream);
+bool flow3_fits(int max_m);
 int flow2_waves_per_cu(int C);
 // workgroups per CU resident for the streamed flow2 kernel cfg selects (ring / slab
 // instantiation, LDS pad of cfg.f2_wgs); -1 on error (sw_flow2.hip)

@@ -1,0 +1,122 @@
+"""GPU parity: the flow3 kernel (sw_flow3.hip: flow2's staged two-column linear-gap
+kernel with hand-scheduled chunk loops, tools/gen_flow3.py) against the oracle,
+bit-exact, and against flow2 (option f3 = 0) on the same inputs.  Ragged shapes
+around the 126-column strip stride, the 4-strip groups and the 64-row chunk pairs,
+every strip role (no inflow / LDS inflow x no outflow / LDS / granules), grids of
+1-3 workgroups (groups run in rounds through the loader's granule path), several
+pairs per launch, three linear-gap constant sets and C2 in full."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ACGT = np.frombuffer(b"ACGT", np.uint8)
+
+
+def _rand_dna(rng, n):
+    return ACGT[rng.integers(0, 4, n)]
+
+
+def _pairs(rng, shapes):
+    out = []
+    for n, m in shapes:
+        a = _rand_dna(rng, n)
+        b = _rand_dna(rng, m)
+        if rng.random() < 0.5 and m > 10:
+            b = np.resize(a, m).copy()        # long diagonals through every strip edge
+            mut = rng.random(m) < 0.05
+            b[mut] = _rand_dna(rng, int(mut.sum()))
+        out.append((a, b))
+    return out
+
+
+@pytest.fixture(autouse=True)
+def _defaults(engine):
+    def reset():
+        engine.set_params(engine.Params())
+        for k in ("W", "C", "blocks", "orient", "f2w"):
+            engine.set_option(k, 0)
+        engine.set_option("mode", -1)
+        engine.set_option("linear", -1)
+        engine.set_option("f3", 1)
+    reset()
+    yield
+    reset()
+
+
+# rows around the 64-row chunk pairs and the ring's 512 rows, columns around the
+# 126-column strips and 504-column groups (1, 2, 4, 5, 8, 9 strips)
+SHAPES = [(1, 1), (1, 200), (200, 1), (2, 5), (126, 127), (128, 63), (129, 64), (130, 65), (252, 95), (253, 96),
+          (254, 97), (505, 505), (506, 511), (1000, 512), (1008, 513), (1009, 1000), (1135, 1100), (2017, 2100),
+          (4096, 4000), (5041, 777)]
+
+
+def test_flow3_ragged(engine, oracle_mod):
+    rng = np.random.default_rng(31)
+    pairs = _pairs(rng, SHAPES)
+    engine.set_option("orient", 1)
+    engine.set_option("mode", 5)      # flow2 planning for every shape (single strips included)
+    engine.set_option("f2w", 2)
+    for prm in (engine.Params(), engine.Params(2, -3, 4, 4), engine.Params(1, 0, 0, 0)):
+        op = oracle_mod.Params(prm.match, prm.mismatch, prm.gap_init, prm.gap_ext)
+        exp = [oracle_mod.score_linear(a, b, op) for a, b in pairs]
+        got = []
+        for a, b in pairs:
+            got.append(engine.score(a, b, prm))
+            st = engine.last_stats()
+            assert st["mode"] == 5 and st["variant"] & 64 and st["variant"] & 16, st
+        assert got == exp, prm
+        assert engine.score_batch(pairs, prm) == exp, prm
+        for blocks in (1, 2, 3):
+            engine.set_option("blocks", blocks)
+            assert engine.score_batch(pairs, prm) == exp, (prm, blocks)
+        engine.set_option("blocks", 0)
+
+
+def test_flow3_matches_flow2(engine):
+    """The same launches on flow2 (option f3 = 0) give the same scores."""
+    rng = np.random.default_rng(32)
+    pairs = _pairs(rng, [(3001, 2999), (6000, 1500), (1500, 6000), (777, 9000)])
+    engine.set_option("mode", 5)      # a batch on the staged flow2 plan (not the streamed item claim)
+    engine.set_option("W", 1)
+    got3 = engine.score_batch(pairs)
+    assert engine.last_stats()["variant"] & 64
+    engine.set_option("f3", 0)
+    got2 = engine.score_batch(pairs)
+    assert not engine.last_stats()["variant"] & 64
+    assert got3 == got2
+
+
+def test_flow3_only_where_it_applies(engine, oracle_mod):
+    """The affine step (G_INIT != G_EXT, or linear = 0) and C = 64 stay on flow2."""
+    rng = np.random.default_rng(33)
+    a, b = _pairs(rng, [(2017, 2100)])[0]
+    prm = engine.Params(2, -3, 5, 2)
+    assert engine.score(a, b, prm) == oracle_mod.score_linear(a, b, oracle_mod.Params(2, -3, 5, 2))
+    assert not engine.last_stats()["variant"] & 64
+    engine.set_option("linear", 0)
+    assert engine.score(a, b) == oracle_mod.score_linear(a, b)
+    assert not engine.last_stats()["variant"] & 64
+    engine.set_option("linear", -1)
+    engine.set_option("C", 64)
+    engine.set_option("mode", 5)
+    assert engine.score(a, b) == oracle_mod.score_linear(a, b)
+    assert not engine.last_stats()["variant"] & 64
+
+
+def test_flow3_config_c2(engine, golden):
+    """C2 (N = 65536, seed 65536) on flow3 against its golden."""
+    import torch
+    c = golden("configs.json")["C2"]
+    N = c["N"]
+    a, b = engine.gen_pair(c["seed"], N)
+    arena = torch.from_numpy(np.concatenate([a, b])).cuda()
+    score = torch.full((1,), -1, dtype=torch.int32, device="cuda")
+    s = torch.cuda.current_stream()
+    for _ in range(3):
+        engine.score_batch_device(arena.data_ptr(), [0], [N], [N], [N], score.data_ptr(), flags=1,
+                                  stream=s.cuda_stream)
+        engine.stream_status(s.cuda_stream)
+        st = engine.last_stats()
+        assert st["mode"] == 5 and st["variant"] & 64 and not st["variant"] & 2, st
+        assert score.item() == c["score"]

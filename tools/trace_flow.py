@@ -41,6 +41,9 @@ def main():
     sw.set_option("W", W)
     sw.set_option("C", C)
     sw.set_option("f2w", f2w)
+    for kv in os.environ.get("TRACE_OPTS", "").split():   # extra engine options k=v
+        k, v = kv.split("=")
+        sw.set_option(k, int(v))
     s = torch.cuda.current_stream()
     for it in range(3):
         if it == 2:
