@@ -275,60 +275,191 @@ def measure_step_ns(sw, torch, arena, offs_a, lens, offs_b, scores, sptr, N):
 
 
 def time_launches(torch, launch, collective, steps, warmup, stream, dist):
+    """Time `steps` launches (+ their collective) between barrier + synchronize brackets;
+    returns (max-over-ranks wall seconds, mean kernel ms from HIP events on `stream`).
+    stream None (CPU ranks of the tests): wall time only, kernel ms None."""
+    gpu = stream is not None
+    sync = torch.cuda.synchronize if gpu else (lambda: None)
     for _ in range(warmup):
         launch()
         collective()
-    torch.cuda.synchronize()
-    starts = [torch.cuda.Event(enable_timing=True) for _ in range(steps)]
-    ends = [torch.cuda.Event(enable_timing=True) for _ in range(steps)]
+    sync()
+    starts = [torch.cuda.Event(enable_timing=True) for _ in range(steps)] if gpu else []
+    ends = [torch.cuda.Event(enable_timing=True) for _ in range(steps)] if gpu else []
     if dist is not None:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     for i in range(steps):
-        starts[i].record(stream)
+        if gpu:
+            starts[i].record(stream)
         launch()
-        ends[i].record(stream)
+        if gpu:
+            ends[i].record(stream)
         collective()
-    torch.cuda.synchronize()
+    sync()
     if dist is not None:
         dist.barrier()
     t_local = time.perf_counter() - t0
-    kern_ms = float(np.mean([s.elapsed_time(e) for s, e in zip(starts, ends)]))
+    kern_ms = float(np.mean([s.elapsed_time(e) for s, e in zip(starts, ends)])) if gpu else None
     t_max = t_local
     if dist is not None:
-        tt = torch.tensor([t_local], dtype=torch.float64, device="cuda")
+        tt = torch.tensor([t_local], dtype=torch.float64, device="cuda" if gpu else "cpu")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         t_max = float(tt.item())
     return t_max, kern_ms
 
 
+class BatchRank:
+    """One rank's share of the batched workload (C3 at one GPU, C4 at eight): the
+    contiguous block shard_bounds(P * world, world, rank) of the global batch (pair k
+    seeded 8192 + k, N x N), scored with no data-path collective; `collective` gathers
+    the int32 scores to rank 0 (RCCL; gloo in the CPU tests).
+    scorer "engine": the HIP kernels on the sequences resident in HBM (sw_score_batch_device);
+    "oracle": the CPU restatement (tests/launch_worker.py runs this class on gloo ranks)."""
+
+    def __init__(self, torch, dist, world, rank, N, P, scorer="engine"):
+        from concurrentproject_amd.dist import shard_bounds
+        self.torch, self.dist, self.world, self.P = torch, dist, world, P
+        self.lo, self.hi = shard_bounds(P * world, world, rank)
+        self.npairs = npairs = self.hi - self.lo
+        self.cells = npairs * N * N
+        self.gathered = None
+        if scorer == "engine":
+            import concurrentproject_amd as sw
+            host = sw.gen_batch(8192 + self.lo, npairs, N)
+            self.arena = torch.from_numpy(host).cuda()
+            self.scores = torch.zeros(npairs, dtype=torch.int32, device="cuda")
+            self.stream = torch.cuda.current_stream()
+            offs_a = [2 * N * k for k in range(npairs)]
+            offs_b = [2 * N * k + N for k in range(npairs)]
+
+            def launch():
+                sw.score_batch_device(self.arena.data_ptr(), offs_a, [N] * npairs, offs_b, [N] * npairs,
+                                      self.scores.data_ptr(), flags=1, stream=self.stream.cuda_stream)
+            self.launch = launch
+        else:
+            import oracle
+            pairs = [oracle.gen_pair(8192 + k, N) for k in range(self.lo, self.hi)]
+            self.scores = torch.zeros(npairs, dtype=torch.int32)
+            self.stream = None
+            self.launch = lambda: self.scores.copy_(torch.tensor(oracle.score_batch(pairs), dtype=torch.int32))
+
+    def collective(self):
+        if self.dist is not None:
+            from concurrentproject_amd.dist import gather_scores
+            self.gathered = gather_scores(self.scores, self.P * self.world)
+
+    def result(self):
+        """Rank 0: every pair's score in global order (a rank without a group: its own)."""
+        if self.gathered is not None:
+            return self.gathered.cpu().tolist()
+        return self.scores.cpu().tolist() if self.dist is None else None
+
+
 def run_batch(sw, torch, dist, world, rank, N, P, steps, warmup):
-    """C3 (one GPU) / C4 (sharded): rank r scores its contiguous block of the global
-    batch, then the per-pair scores are gathered to rank 0 (RCCL) every step."""
-    from concurrentproject_amd.dist import gather_scores, shard_bounds
-    lo, hi = shard_bounds(P * world, world, rank)
-    host = sw.gen_batch(8192 + lo, hi - lo, N)
-    npairs = hi - lo
-    arena = torch.from_numpy(host).cuda()
-    scores = torch.zeros(npairs, dtype=torch.int32, device="cuda")
-    stream = torch.cuda.current_stream()
-    offs_a = [2 * N * k for k in range(npairs)]
-    offs_b = [2 * N * k + N for k in range(npairs)]
-    gathered = [None]
+    """C3 (one GPU) / C4 (sharded): BatchRank timed over `steps` launches."""
+    job = BatchRank(torch, dist, world, rank, N, P)
+    t_max, kern_ms = time_launches(torch, job.launch, job.collective, steps, warmup, job.stream, dist)
+    sw.stream_status(job.stream.cuda_stream)
+    return t_max, kern_ms, job.result(), job.cells, sw.last_stats()
 
-    def launch():
-        sw.score_batch_device(arena.data_ptr(), offs_a, [N] * npairs, offs_b, [N] * npairs, scores.data_ptr(),
-                              flags=1, stream=stream.cuda_stream)
 
-    def collective():
-        if dist is not None:
-            gathered[0] = gather_scores(scores, P * world)
+class OracleSlabs:
+    """The CPU stand-in of dist.ColumnSlabs in the gloo tests: the same bounds
+    (sw_slab_bounds), the same all-reduce(MAX) of one int, with the edge column
+    passed rank to rank by gloo send/recv in place of the kernel's IPC stores."""
 
-    t_max, kern_ms = time_launches(torch, launch, collective, steps, warmup, stream, dist)
-    sw.stream_status(stream.cuda_stream)
-    allsc = gathered[0].cpu().tolist() if gathered[0] is not None else scores.cpu().tolist()
-    return t_max, kern_ms, allsc, npairs * N * N, sw.last_stats()
+    def __init__(self, dist, n, m, a, b):
+        import concurrentproject_amd as sw
+        self.dist, self.n, self.m, self.a, self.b = dist, n, m, a, b
+        self.rank, self.world = dist.get_rank(), dist.get_world_size()
+        self.bounds = sw.slab_bounds(n, m, self.world, sw.SW_FLAG_DNA)
+        self.inflow = None
+
+    @property
+    def columns(self):
+        return self.bounds[self.rank], self.bounds[self.rank + 1]
+
+    def launch(self):
+        import oracle
+        import torch
+        lo, hi = self.columns
+        edge = None
+        if self.rank > 0:
+            eh, ee = torch.empty(self.m, dtype=torch.int32), torch.empty(self.m, dtype=torch.int32)
+            self.dist.recv(eh, src=self.rank - 1)
+            self.dist.recv(ee, src=self.rank - 1)
+            edge = (eh.numpy(), ee.numpy())
+        best, (oh, oe) = oracle.slab(self.a[lo:hi], self.b, edge=edge)
+        if self.rank + 1 < self.world:
+            self.dist.send(torch.from_numpy(np.ascontiguousarray(oh)), dst=self.rank + 1)
+            self.dist.send(torch.from_numpy(np.ascontiguousarray(oe)), dst=self.rank + 1)
+        self.score = torch.tensor([best], dtype=torch.int32)
+
+    def reduce(self):
+        from concurrentproject_amd.dist import slab_max
+        return slab_max(self.score)
+
+    def close(self):
+        pass
+
+
+class SlabRank:
+    """One rank's slab of the C5 pair cut into column slabs (f-1): `launch` scores it
+    (dist.ColumnSlabs: the kernel stores its right edge into the next rank's IPC-mapped
+    fine-grained buffer, and the all-reduce(MAX) of the slab maxima follows on the same
+    stream); `report` gathers the per-rank kernel times, columns, pipeline fill and
+    inflow memory kinds.  scorer "oracle": OracleSlabs on gloo (tests)."""
+
+    def __init__(self, torch, dist, n, m, a, b, scorer="engine"):
+        self.torch, self.dist = torch, dist
+        self.world, self.rank = dist.get_world_size(), dist.get_rank()
+        self.score = None
+        if scorer == "engine":
+            import concurrentproject_amd as sw
+            from concurrentproject_amd.dist import ColumnSlabs
+            self.arena = torch.from_numpy(np.concatenate([a, b])).cuda()
+            self.slabs = ColumnSlabs(n, m, sw.SW_FLAG_DNA)
+            self.stream = torch.cuda.current_stream()
+            self.launch = lambda: self.slabs.launch(self.arena.data_ptr(), 0, n, self.stream.cuda_stream)
+        else:
+            self.slabs = OracleSlabs(dist, n, m, a, b)
+            self.stream = None
+            self.launch = self.slabs.launch
+        inflow = self.slabs.inflow
+        self.fine_grained = inflow.fine_grained if inflow is not None else None
+        lo, hi = self.slabs.columns
+        self.cells = (hi - lo) * m
+
+    def collective(self):
+        """The all-reduce(MAX) of the slab maxima (RCCL; after the kernel's event, so the
+        per-rank kernel times keep the pipeline fill)."""
+        self.score = self.slabs.reduce()
+
+    def report(self, kern_ms):
+        """Every rank's launch-to-end kernel time (rank r's includes its wait for rank r-1's
+        first edge rows: last - first is the pipeline fill), columns and inflow memory kind."""
+        torch, dist, world = self.torch, self.dist, self.world
+        kind = {None: -1.0, True: 1.0, False: 0.0}[self.fine_grained]
+        kt = torch.tensor([kern_ms if kern_ms is not None else -1.0, kind], dtype=torch.float64,
+                          device="cuda" if self.stream is not None else "cpu")
+        allk = [torch.zeros_like(kt) for _ in range(world)]
+        dist.all_gather(allk, kt)
+        per_rank = [round(float(x[0].item()), 4) for x in allk]
+        b = self.slabs.bounds
+        return {"per_rank_kernel_ms": per_rank, "per_rank_columns": [b[r + 1] - b[r] for r in range(world)],
+                "pipeline_fill_ms": round(per_rank[-1] - per_rank[0], 4),
+                "inflow_fine_grained": [{1.0: True, 0.0: False}.get(float(x[1].item())) for x in allk],
+                "note": "rank 0 runs at its own pace; rank r's kernel also waits for the first edge rows of rank "
+                        "r-1, so last - first is the fill of the R-1 hops; inflow_fine_grained: each rank's inflow "
+                        "buffer (rank 0 has none; an edge written by another GPU needs fine-grained memory)"}
+
+    def result(self):
+        return int(self.score[0].item())
+
+    def close(self):
+        self.slabs.close()
 
 
 def start_ranks(args) -> int | None:
@@ -431,10 +562,9 @@ def main():
         offs_a, offs_b, lens = [0], [N], [N]
         cells_rank = cells_job = N * N
         if workload == "slab" and dist is not None:
-            from concurrentproject_amd.dist import ColumnSlabs
-            slabs = ColumnSlabs(N, N, sw.SW_FLAG_DNA)
-            lo, hi = slabs.columns
-            cells_rank, cells_job = (hi - lo) * N, N * N
+            slabs = SlabRank(torch, dist, N, N, a, b)
+            lo, hi = slabs.slabs.columns
+            cells_rank, cells_job = slabs.cells, N * N
             cfg["slab_columns"] = [lo, hi]
         elif workload == "slab" and args.slab_of > 1:
             bounds = sw.slab_bounds(N, N, args.slab_of, sw.SW_FLAG_DNA)
@@ -450,10 +580,7 @@ def main():
 
         def launch():
             if slabs is not None:
-                epoch[0] += 1
-                lo, hi = slabs.columns
-                sw.score_slab_device(arena.data_ptr(), lo, hi - lo, N, N, slabs.inflow.ptr if slabs.inflow else 0,
-                                     slabs.outflow, slabs.epoch + epoch[0], scores.data_ptr(), sw.SW_FLAG_DNA, sptr)
+                slabs.launch()
             elif slab_buf is not None:
                 epoch[0] += 1
                 sw.score_slab_device(arena.data_ptr(), 0, slab_cols, N, N, 0, slab_buf.ptr, epoch[0],
@@ -466,8 +593,7 @@ def main():
             if dist is None:
                 return
             if slabs is not None:
-                from concurrentproject_amd.dist import slab_max
-                slab_max(scores)                           # RCCL all-reduce(MAX) of one int
+                slabs.collective()                         # RCCL all-reduce(MAX) of one int
             else:
                 from concurrentproject_amd.dist import gather_scores
                 gathered[0] = gather_scores(scores, world)  # RCCL gather of the per-pair int32 scores
@@ -477,17 +603,8 @@ def main():
         st = sw.last_stats()
         first = gathered[0][0].item() if gathered[0] is not None else scores[0].item()
         if slabs is not None:
-            # every rank's launch-to-end kernel time: rank r's includes the wait for
-            # rank r-1's edge, so the spread over ranks is the pipeline fill
-            kt = torch.tensor([avg_kern_ms], dtype=torch.float64, device="cuda")
-            allk = [torch.zeros_like(kt) for _ in range(world)]
-            dist.all_gather(allk, kt)
-            per_rank = [round(float(x.item()), 4) for x in allk]
-            slab_ranks = {"per_rank_kernel_ms": per_rank,
-                          "per_rank_columns": [slabs.bounds[r + 1] - slabs.bounds[r] for r in range(world)],
-                          "pipeline_fill_ms": round(per_rank[-1] - per_rank[0], 4),
-                          "note": "rank 0 runs at its own pace; rank r's kernel also waits for the first "
-                                  "edge rows of rank r-1, so last - first is the fill of the R-1 hops"}
+            first = slabs.result()
+            slab_ranks = slabs.report(avg_kern_ms)
             slabs.close()
         if slab_buf is not None:
             slab_buf.free()

@@ -106,6 +106,11 @@ def lib() -> ctypes.CDLL:
     L.sw_score_batch.argtypes = [ctypes.POINTER(u8p), ctypes.POINTER(i), ctypes.POINTER(u8p),
                                  ctypes.POINTER(i), i, ctypes.POINTER(i)]
     L.sw_score_batch.restype = i
+    L.sw_score_batch_multi.argtypes = [ctypes.POINTER(u8p), ctypes.POINTER(i), ctypes.POINTER(u8p),
+                                       ctypes.POINTER(i), i, ctypes.POINTER(i), i]
+    L.sw_score_batch_multi.restype = i
+    L.sw_batch_shard.argtypes = [i, i, i, ctypes.POINTER(i), ctypes.POINTER(i)]
+    L.sw_batch_shard.restype = i
     L.sw_score_batch_device.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(i),
                                         ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(i), i, ctypes.c_void_p, i,
                                         ctypes.c_void_p]
@@ -214,8 +219,10 @@ def score(seq1, seq2, params: Params | None = None) -> int:
                                         params.gap_init, params.gap_ext))
 
 
-def score_batch(pairs: Iterable[Sequence], params: Params | None = None) -> list:
-    """Scores of many independent pairs in one launch."""
+def score_batch(pairs: Iterable[Sequence], params: Params | None = None, ngpus: int = 0) -> list:
+    """Scores of many independent pairs in one launch (sw_score_batch); with ngpus >= 1,
+    sharded over the first ngpus GPUs with an RCCL gather of the scores
+    (sw_score_batch_multi)."""
     arrs = [(_u8(a), _u8(b)) for a, b in pairs]
     n = len(arrs)
     if n == 0:
@@ -231,11 +238,21 @@ def score_batch(pairs: Iterable[Sequence], params: Params | None = None) -> list
         old = get_params()
         set_params(params)
     try:
-        _check(lib().sw_score_batch(A, AL, B, BL, n, out))
+        if ngpus:
+            _check(lib().sw_score_batch_multi(A, AL, B, BL, n, out, ngpus))
+        else:
+            _check(lib().sw_score_batch(A, AL, B, BL, n, out))
     finally:
         if old is not None:
             set_params(old)
     return list(out)
+
+
+def batch_shard(npairs: int, ngpus: int, rank: int) -> tuple:
+    """[lo, hi) of rank `rank`'s contiguous shard in sw_score_batch_multi (no GPU call)."""
+    lo, hi = ctypes.c_int(), ctypes.c_int()
+    _check(lib().sw_batch_shard(npairs, ngpus, rank, ctypes.byref(lo), ctypes.byref(hi)))
+    return lo.value, hi.value
 
 
 def score_batch_device(d_arena_ptr: int, a_off, alen, b_off, blen, d_scores_ptr: int, flags: int = 0,

@@ -13,9 +13,15 @@
 #include "sw_internal.h"
 #include "../../include/algoGPU.h"
 
+#include <rccl/rccl.h>
+#include <dlfcn.h>
+
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
+#include <functional>
+#include <thread>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -58,7 +64,7 @@ Params g_params;
 
 std::atomic<long long> g_opt_W{0}, g_opt_C{0}, g_opt_bytes{0}, g_opt_timeout{30}, g_opt_blocks{0}, g_opt_orient{0},
     g_opt_mode{-1}, g_opt_trace{0}, g_opt_duo_f16{1}, g_opt_f2stream{0}, g_opt_ring{-1}, g_opt_ring_rows{4096}, g_opt_f2_wgs{0}, g_opt_f2w{0}, g_opt_f2pwg{-1},
-    g_opt_linear{-1}, g_opt_f3{1};
+    g_opt_linear{-1}, g_opt_f3{1}, g_opt_slab_plain{0};
 
 // Longest sequence the engine takes: granule buffers of m rows keep m * 16 in the
 // 32-bit record count of a buffer resource (sw_device.h linear_edge).
@@ -386,7 +392,10 @@ void plan_flow2(Job& job, bool w2, bool pwg = false) {
 bool pwg_fits(const Job& job, const Params& prm, int wgs) {
     int max_m = 0;
     for (const PairDesc& d : job.pairs) max_m = std::max(max_m, d.m);
-    return flow2_pwg_wgs(max_m, 64, flow2_w2_wanted(job, prm)) >= wgs;
+    const bool lin = flow2_w2_wanted(job, prm);
+    // the round buffer must also pass the launch's dynamic-LDS limit (sw_flow2.hip flow2_dyn_lds)
+    return flow2_pwg_wgs(max_m, 64, lin) >= wgs &&
+           flow2_pwg_row_bytes(lin) * flow2_pwg_rows(max_m, 64) <= flow2_stream_dyn_max(64);
 }
 
 // A batch on the pair-per-workgroup flow2 kernel: W = 1 strips, 64-row chunks, streamed
@@ -613,10 +622,14 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
     if (f2s) {
         const long long o = g_opt_f2_wgs.load();
         const int per_cu = job.item_base[np] / c->cus;
+        // a pair per workgroup: every pair resident in one pass when the LDS admits it
+        // (ceil: cus < P < 2 cus needs 2 per CU, not a second pass of P - cus pairs)
+        const int per_cu_ceil = (job.item_base[np] + c->cus - 1) / c->cus;
         f2_wgs = o > 0           ? (int)o
                  : job.ring      ? (job.item_base[np] <= c->cus * F2_WGS_MAX ? F2_WGS_MAX
                                                                              : std::min(F2_WGS_MAX, std::max(1, per_cu / 2)))
-                 : job.pwg       ? std::min({F2_WGS_MAX, std::max(1, per_cu), flow2_pwg_wgs(max_m_all, job.C, job.f2w2)})
+                 : job.pwg       ? std::min({F2_WGS_MAX, std::max(1, per_cu_ceil),
+                                             flow2_pwg_wgs(max_m_all, job.C, job.f2w2)})
                  : per_cu >= 4   ? 2
                                  : 1;
     }
@@ -815,10 +828,9 @@ struct HostPair {
     int m;   // seq2 length (reference: rows)
 };
 
-// Synchronous host-buffer path shared by every host API entry.
-int score_host(const HostPair* in, int npairs, const Params& prm, int* out) {
-    const auto t0 = std::chrono::steady_clock::now();
-    if (npairs < 0 || (npairs > 0 && (!in || !out))) {
+// Host pairs validated for the engine (lengths, pointers, score range).
+int check_host_pairs(const HostPair* in, int npairs, const Params& prm) {
+    if (npairs < 0 || (npairs > 0 && !in)) {
         set_err("invalid arguments");
         return -1;
     }
@@ -836,18 +848,17 @@ int score_host(const HostPair* in, int npairs, const Params& prm, int* out) {
             set_err("pair %d: sequences longer than 2^27 - 1 bytes are not supported", k);
             return -1;
         }
-        out[k] = 0;   // empty pairs score 0 (main.cpp:74-90 with empty loops)
     }
-    std::vector<int> act;
-    for (int k = 0; k < npairs; ++k)
-        if (in[k].n > 0 && in[k].m > 0) act.push_back(k);
-    if (act.empty()) return 0;
+    return 0;
+}
 
-    Ctx* c = get_ctx();
-    if (!c) return -1;
+// Stage the non-empty pairs in[act[i]] and launch them on c's own stream (asynchronous).
+// Pair act[i]'s score goes to d_scores[full ? act[i] : i]; enqueue zeroes the nscores
+// ints of d_scores first, so empty pairs of a full-index launch read 0.
+int launch_host(Ctx* c, const HostPair* in, const std::vector<int>& act, const Params& prm, int* d_scores,
+                int nscores, bool full) {
     hipStream_t s = c->own;
     if (c->last && c->last != s) HIPCHK(hipStreamSynchronize(c->last));
-
     Job job;
     const bool single = act.size() == 1;
     bool dna = g_opt_bytes.load() == 0;
@@ -878,14 +889,35 @@ int score_host(const HostPair* in, int npairs, const Params& prm, int* out) {
         off += ((size_t)m + 15) / 16 * 16;
         d.n = n;
         d.m = m;
-        d.out_idx = (int)i;
+        d.out_idx = full ? act[i] : (int)i;
     }
     const int W = pick_W(job.pairs, single);
     plan(job, W, pick_C(W), single);
     if (finalize_mode(job, prm, c->cus)) return -1;
-    if (c->seq.ensure(bytes, s) || c->scores.ensure(act.size(), s) || c->hscores.ensure(act.size())) return -1;
+    if (c->seq.ensure(bytes, s)) return -1;
     HIPCHK(hipMemcpyAsync(c->seq.p, c->hseq.p, bytes, hipMemcpyHostToDevice, s));
-    if (enqueue(c, job, prm, c->seq.p, c->scores.p, (int)act.size(), s, true)) return -1;
+    return enqueue(c, job, prm, c->seq.p, d_scores, nscores, s, true);
+}
+
+// Synchronous host-buffer path shared by every host API entry.
+int score_host(const HostPair* in, int npairs, const Params& prm, int* out) {
+    const auto t0 = std::chrono::steady_clock::now();
+    if (npairs > 0 && !out) {
+        set_err("invalid arguments");
+        return -1;
+    }
+    if (check_host_pairs(in, npairs, prm)) return -1;
+    std::vector<int> act;
+    for (int k = 0; k < npairs; ++k) {
+        out[k] = 0;   // empty pairs score 0 (main.cpp:74-90 with empty loops)
+        if (in[k].n > 0 && in[k].m > 0) act.push_back(k);
+    }
+    if (act.empty()) return 0;
+    Ctx* c = get_ctx();
+    if (!c) return -1;
+    hipStream_t s = c->own;
+    if (c->scores.ensure(act.size(), s) || c->hscores.ensure(act.size())) return -1;
+    if (launch_host(c, in, act, prm, c->scores.p, (int)act.size(), false)) return -1;
     HIPCHK(hipMemcpyAsync(c->hscores.p, c->scores.p, act.size() * sizeof(int), hipMemcpyDeviceToHost, s));
     if (check_ctrl(c, s)) return -1;   // synchronises
     float ms = 0.f;
@@ -893,6 +925,29 @@ int score_host(const HostPair* in, int npairs, const Params& prm, int* out) {
     for (size_t i = 0; i < act.size(); ++i) out[act[i]] = c->hscores.p[i];
     t_stats.kernel_ms = ms;
     t_stats.total_ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return 0;
+}
+
+// One device's shard of a multi-GPU batch (sw_score_batch_multi): the scores of
+// in[0..npairs) stay in device memory, *d_out (npairs ints of this thread's context).
+int score_host_device(const HostPair* in, int npairs, const Params& prm, int** d_out, float* kernel_ms) {
+    *kernel_ms = 0.f;
+    Ctx* c = get_ctx();
+    if (!c) return -1;
+    hipStream_t s = c->own;
+    if (c->scores.ensure((size_t)std::max(npairs, 1), s)) return -1;
+    *d_out = c->scores.p;
+    std::vector<int> act;
+    for (int k = 0; k < npairs; ++k)
+        if (in[k].n > 0 && in[k].m > 0) act.push_back(k);
+    if (act.empty()) {
+        if (npairs > 0) HIPCHK(hipMemsetAsync(c->scores.p, 0, (size_t)npairs * sizeof(int), s));
+        HIPCHK(hipStreamSynchronize(s));
+        return 0;
+    }
+    if (launch_host(c, in, act, prm, c->scores.p, npairs, true)) return -1;
+    if (check_ctrl(c, s)) return -1;   // synchronises
+    HIPCHK(hipEventElapsedTime(kernel_ms, c->ev0, c->ev1));
     return 0;
 }
 
@@ -928,6 +983,217 @@ __global__ void alphabet_kernel(const unsigned char* arena, const PairDesc* pair
 
 // the thread's sw_last_error() text, for the other host modules (sw_db.hip)
 void report_error(const char* msg) { set_err("%s", msg); }
+
+// ---- multi-GPU batch (sw_score_batch_multi) ---------------------------------
+// Contiguous shard of pair rank r of ngpus (sizes differ by <= 1): the partition of
+// concurrentproject_amd/dist.py shard_bounds.
+void batch_shard(int npairs, int ngpus, int r, int* lo, int* hi) {
+    const int base = npairs / ngpus, extra = npairs % ngpus;
+    *lo = r * base + std::min(r, extra);
+    *hi = *lo + base + (r < extra ? 1 : 0);
+}
+
+// RCCL, loaded at first use (dlopen: the library has no link-time RCCL dependency, and a
+// process that already holds librccl.so.1 -- PyTorch's -- shares that copy).
+struct Rccl {
+    bool tried = false, ok = false;
+    std::string why;
+    ncclResult_t (*comm_init_all)(ncclComm_t*, int, const int*) = nullptr;
+    ncclResult_t (*group_start)() = nullptr;
+    ncclResult_t (*group_end)() = nullptr;
+    ncclResult_t (*send)(const void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*recv)(void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    const char* (*err)(ncclResult_t) = nullptr;
+    bool load() {
+        if (tried) return ok;
+        tried = true;
+        void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) {
+            why = std::string("dlopen librccl.so.1: ") + dlerror();
+            return false;
+        }
+        comm_init_all = (decltype(comm_init_all))dlsym(h, "ncclCommInitAll");
+        group_start = (decltype(group_start))dlsym(h, "ncclGroupStart");
+        group_end = (decltype(group_end))dlsym(h, "ncclGroupEnd");
+        send = (decltype(send))dlsym(h, "ncclSend");
+        recv = (decltype(recv))dlsym(h, "ncclRecv");
+        err = (decltype(err))dlsym(h, "ncclGetErrorString");
+        ok = comm_init_all && group_start && group_end && send && recv && err;
+        if (!ok) why = "librccl.so.1 lacks ncclCommInitAll/ncclGroupStart/ncclGroupEnd/ncclSend/ncclRecv";
+        return ok;
+    }
+};
+
+// One host thread per device, created once: its thread-local engine context (stream,
+// buffers) then lives as long as the process, like a caller's own thread.
+struct DevWorker {
+    std::thread th;
+    std::mutex mu;
+    std::condition_variable cv;
+    std::function<void()> job;
+    bool busy = false;
+    void start() {
+        th = std::thread([this] {
+            for (;;) {
+                std::function<void()> f;
+                {
+                    std::unique_lock<std::mutex> g(mu);
+                    cv.wait(g, [this] { return busy && job; });
+                    f = std::move(job);
+                }
+                f();
+                {
+                    std::lock_guard<std::mutex> g(mu);
+                    busy = false;
+                }
+                cv.notify_all();
+            }
+        });
+        th.detach();
+    }
+    void post(std::function<void()> f) {
+        std::lock_guard<std::mutex> g(mu);
+        job = std::move(f);
+        busy = true;
+        cv.notify_all();
+    }
+    void wait() {
+        std::unique_lock<std::mutex> g(mu);
+        cv.wait(g, [this] { return !busy; });
+    }
+};
+
+struct MultiState {
+    std::mutex mu;                          // one multi-GPU call at a time
+    Rccl rccl;
+    std::vector<DevWorker*> workers;        // per device
+    std::map<int, std::vector<ncclComm_t>> comms;   // ngpus -> communicator clique of devices 0..ngpus-1
+    std::vector<hipStream_t> streams;       // per device, for the gather
+    int* d_gather = nullptr;                // device 0
+    size_t gather_cap = 0;
+    int* h_scores = nullptr;                // pinned
+    size_t h_cap = 0;
+};
+MultiState& multi_state() {
+    static MultiState* st = new MultiState();   // never destroyed: detached workers use it
+    return *st;
+}
+
+#define NCCLCHK(expr)                                                                   \
+    do {                                                                                \
+        ncclResult_t r_ = (expr);                                                       \
+        if (r_ != ncclSuccess) {                                                        \
+            set_err("%s failed: %s", #expr, st.rccl.err ? st.rccl.err(r_) : "rccl");   \
+            return -1;                                                                  \
+        }                                                                               \
+    } while (0)
+
+int score_multi(const HostPair* in, int npairs, const Params& prm, int* out, int ngpus) {
+    const auto t0 = std::chrono::steady_clock::now();
+    int ndev = 0;
+    HIPCHK(hipGetDeviceCount(&ndev));
+    if (ngpus < 1 || ngpus > ndev) {
+        set_err("sw_score_batch_multi: ngpus = %d, but %d HIP device(s) are visible", ngpus, ndev);
+        return -1;
+    }
+    if (npairs > 0 && !out) {
+        set_err("invalid arguments");
+        return -1;
+    }
+    if (check_host_pairs(in, npairs, prm)) return -1;
+    if (npairs == 0) return 0;
+    MultiState& st = multi_state();
+    std::lock_guard<std::mutex> g(st.mu);
+    if (ngpus > 1 && !st.rccl.load()) {
+        set_err("sw_score_batch_multi: %s", st.rccl.why.c_str());
+        return -1;
+    }
+    while ((int)st.workers.size() < ngpus) {
+        st.workers.push_back(new DevWorker());
+        st.workers.back()->start();
+    }
+    // every device scores its contiguous shard on its own host thread and stream
+    std::vector<int> rc(ngpus, 0), lo(ngpus), hi(ngpus);
+    std::vector<int*> dptr(ngpus, nullptr);
+    std::vector<float> kms(ngpus, 0.f);
+    std::vector<std::string> errs(ngpus);
+    for (int r = 0; r < ngpus; ++r) {
+        batch_shard(npairs, ngpus, r, &lo[r], &hi[r]);
+        st.workers[r]->post([&, r] {
+            if (hipSetDevice(r) != hipSuccess) {
+                rc[r] = -1;
+                errs[r] = "hipSetDevice failed";
+                return;
+            }
+            rc[r] = score_host_device(in + lo[r], hi[r] - lo[r], prm, &dptr[r], &kms[r]);
+            if (rc[r]) errs[r] = t_err;
+        });
+    }
+    for (int r = 0; r < ngpus; ++r) st.workers[r]->wait();
+    for (int r = 0; r < ngpus; ++r)
+        if (rc[r]) {
+            set_err("sw_score_batch_multi: device %d: %s", r, errs[r].c_str());
+            return -1;
+        }
+    int dev0 = 0;
+    HIPCHK(hipGetDevice(&dev0));
+    while ((int)st.streams.size() < ngpus) {
+        HIPCHK(hipSetDevice((int)st.streams.size()));
+        hipStream_t sx = nullptr;
+        HIPCHK(hipStreamCreateWithFlags(&sx, hipStreamNonBlocking));
+        st.streams.push_back(sx);
+    }
+    HIPCHK(hipSetDevice(0));
+    if ((size_t)npairs > st.gather_cap) {
+        if (st.d_gather) HIPCHK(hipFree(st.d_gather));
+        if (st.h_scores) HIPCHK(hipHostFree(st.h_scores));
+        st.d_gather = nullptr;
+        st.h_scores = nullptr;
+        st.gather_cap = 0;
+        HIPCHK(hipMalloc((void**)&st.d_gather, (size_t)npairs * sizeof(int)));
+        HIPCHK(hipHostMalloc((void**)&st.h_scores, (size_t)npairs * sizeof(int), hipHostMallocDefault));
+        st.gather_cap = (size_t)npairs;
+    }
+    // device 0's own shard, then the others' int32 scores over RCCL (the only exchange)
+    if (hi[0] > lo[0])
+        HIPCHK(hipMemcpyAsync(st.d_gather, dptr[0], (size_t)(hi[0] - lo[0]) * sizeof(int), hipMemcpyDeviceToDevice,
+                              st.streams[0]));
+    if (ngpus > 1) {
+        auto it = st.comms.find(ngpus);
+        if (it == st.comms.end()) {
+            std::vector<ncclComm_t> cl(ngpus);
+            std::vector<int> devs(ngpus);
+            for (int r = 0; r < ngpus; ++r) devs[r] = r;
+            NCCLCHK(st.rccl.comm_init_all(cl.data(), ngpus, devs.data()));
+            it = st.comms.emplace(ngpus, cl).first;
+        }
+        const std::vector<ncclComm_t>& cl = it->second;
+        NCCLCHK(st.rccl.group_start());
+        for (int r = 1; r < ngpus; ++r) {
+            const size_t cnt = (size_t)(hi[r] - lo[r]);
+            if (!cnt) continue;
+            NCCLCHK(st.rccl.send(dptr[r], cnt, ncclInt32, 0, cl[r], st.streams[r]));
+            NCCLCHK(st.rccl.recv(st.d_gather + lo[r], cnt, ncclInt32, r, cl[0], st.streams[0]));
+        }
+        NCCLCHK(st.rccl.group_end());
+    }
+    HIPCHK(hipSetDevice(0));
+    HIPCHK(hipMemcpyAsync(st.h_scores, st.d_gather, (size_t)npairs * sizeof(int), hipMemcpyDeviceToHost,
+                          st.streams[0]));
+    for (int r = 0; r < ngpus; ++r) {
+        HIPCHK(hipSetDevice(r));
+        HIPCHK(hipStreamSynchronize(st.streams[r]));
+    }
+    HIPCHK(hipSetDevice(dev0));
+    std::memcpy(out, st.h_scores, (size_t)npairs * sizeof(int));
+    t_stats = sw_stats{};
+    for (int r = 0; r < ngpus; ++r) t_stats.kernel_ms = std::max(t_stats.kernel_ms, kms[r]);
+    for (int k = 0; k < npairs; ++k) t_stats.cells += (long long)in[k].n * in[k].m;
+    t_stats.total_ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return 0;
+}
+#undef NCCLCHK
 
 hipError_t raise_dyn_lds(const void* fn, int bytes) {
     static std::mutex mu;
@@ -1005,6 +1271,26 @@ int sw_score_batch(const unsigned char* const* a, const int* alen, const unsigne
     std::vector<HostPair> v((size_t)npairs);
     for (int k = 0; k < npairs; ++k) v[k] = HostPair{a[k], alen[k], b[k], blen[k]};
     return score_host(v.data(), npairs, current_params(), scores_out);
+}
+
+int sw_score_batch_multi(const unsigned char* const* a, const int* alen, const unsigned char* const* b,
+                         const int* blen, int npairs, int* scores_out, int ngpus) {
+    if (npairs < 0 || (npairs > 0 && (!a || !alen || !b || !blen || !scores_out))) {
+        set_err("sw_score_batch_multi: invalid arguments");
+        return -1;
+    }
+    std::vector<HostPair> v((size_t)npairs);
+    for (int k = 0; k < npairs; ++k) v[k] = HostPair{a[k], alen[k], b[k], blen[k]};
+    return score_multi(v.data(), npairs, current_params(), scores_out, ngpus);
+}
+
+int sw_batch_shard(int npairs, int ngpus, int rank, int* lo, int* hi) {
+    if (npairs < 0 || ngpus < 1 || rank < 0 || rank >= ngpus || !lo || !hi) {
+        set_err("sw_batch_shard: invalid arguments");
+        return -1;
+    }
+    batch_shard(npairs, ngpus, rank, lo, hi);
+    return 0;
 }
 
 int sw_score_batch_device(const unsigned char* d_arena, const int64_t* a_off, const int* alen, const int64_t* b_off,
@@ -1165,16 +1451,24 @@ int sw_slab_alloc(int m, void** d_buf, void* ipc_handle) {
         return -1;
     }
     const size_t bytes = (size_t)m * sizeof(Granule);
-    // fine-grained: coherent for a peer GPU's writes while the consuming kernel
-    // polls; plain device memory if the driver cannot export fine-grained memory
-    for (int kind = 1; kind <= 2; ++kind) {
+    // fine-grained: coherent for a peer GPU's writes while the consuming kernel polls
+    // (DESIGN.md section 7).  A buffer exported for another process (ipc_handle) is the
+    // inflow of a cross-GPU slab edge: it must be fine-grained, and the plain-memory
+    // fallback is refused unless option slab_plain = 1 (one-GPU tests only); a buffer
+    // of this process alone may fall back to plain device memory.
+    const int last_kind = ipc_handle && !g_opt_slab_plain.load() ? 1 : 2;
+    for (int kind = 1; kind <= last_kind; ++kind) {
         void* p = nullptr;
         const hipError_t e = kind == 1 ? hipExtMallocWithFlags(&p, bytes, hipDeviceMallocFinegrained)
                                        : hipMalloc(&p, bytes);
         if (e != hipSuccess) {
             (void)hipGetLastError();
-            if (kind == 2) {
-                set_err("sw_slab_alloc: %s", hipGetErrorString(e));
+            if (kind == last_kind) {
+                set_err(kind == 1 ? "sw_slab_alloc: fine-grained device memory unavailable (%s): a slab edge "
+                                    "written by another GPU needs it (option slab_plain = 1 allows plain memory "
+                                    "for one-GPU tests)"
+                                  : "sw_slab_alloc: %s",
+                        hipGetErrorString(e));
                 return -1;
             }
             continue;
@@ -1186,8 +1480,12 @@ int sw_slab_alloc(int m, void** d_buf, void* ipc_handle) {
             if (ei != hipSuccess) {
                 (void)hipGetLastError();
                 (void)hipFree(p);
-                if (kind == 2) {
-                    set_err("hipIpcGetMemHandle failed: %s", hipGetErrorString(ei));
+                if (kind == last_kind) {
+                    set_err(kind == 1 ? "sw_slab_alloc: fine-grained memory cannot be exported (hipIpcGetMemHandle: "
+                                        "%s): a slab edge written by another GPU needs it (option slab_plain = 1 "
+                                        "allows plain memory for one-GPU tests)"
+                                      : "hipIpcGetMemHandle failed: %s",
+                            hipGetErrorString(ei));
                     return -1;
                 }
                 continue;
@@ -1273,6 +1571,9 @@ int sw_set_option(const char* key, long long v) {
     } else if (k == "f3") {   // 1 (default): staged W2 linear-gap launches on flow3 (sw_flow3.hip), 0: flow2
         if (v < 0 || v > 1) return -1;
         g_opt_f3 = v;
+    } else if (k == "slab_plain") {   // 1: exported slab buffers may fall back to plain device memory
+        if (v < 0 || v > 1) return -1;
+        g_opt_slab_plain = v;
     } else if (k == "ring") {   // flow2 one-pair group edges: -1 auto (rings above 1 GB of edges), 0 off, 1 on
         if (v < -1 || v > 1) return -1;
         g_opt_ring = v;
@@ -1306,6 +1607,7 @@ long long sw_get_option(const char* key) {
     if (k == "f2w") return g_opt_f2w;
     if (k == "f2pwg") return g_opt_f2pwg;
     if (k == "f3") return g_opt_f3;
+    if (k == "slab_plain") return g_opt_slab_plain;
     return -1;
 }
 

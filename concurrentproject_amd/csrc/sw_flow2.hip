@@ -815,7 +815,8 @@ template <int C, bool STREAM>
 int flow2_dyn_lds(const LaunchCfg& cfg, int* lim) {
     const int wgs = STREAM ? std::max(1, std::min(cfg.f2_wgs, F2_WGS_MAX)) : 1;
     const int pad = LDS_PER_CU / (wgs + 1) + 1024 - flow2_static_lds(C, f2_loader<STREAM>() ? 5 : 4);
-    *lim = flow2_stage_max(C) - (STREAM ? 4 * (F2_CR + C + 64) : 0);
+    static_assert(F2_CR == 256, "flow2_stream_dyn_max assumes 256-row code rings");
+    *lim = STREAM ? flow2_stream_dyn_max(C) : flow2_stage_max(C);
     if (STREAM && cfg.f2_pwg)   // the round buffer
         return std::max(pad, flow2_pwg_row_bytes(cfg.f2_lin) * flow2_pwg_rows(cfg.max_m, C));
     return STREAM ? pad : std::max(flow2_stage_bytes(cfg.max_m, C), pad);

@@ -160,6 +160,9 @@ __host__ __device__ constexpr int flow2_stage_bytes(int m, int C) {
 // (rings: 4, or 5 with the staged kernel's loader wave, whose static LDS bounds the staged rows)
 __host__ __device__ constexpr int flow2_static_lds(int C, int rings = 5) { return rings * (256 * 8 + 64 * 8 + 64 * 4) + 64 + 0 * C; }
 __host__ __device__ constexpr int flow2_stage_max(int C) { return LDS_PER_CU - flow2_static_lds(C) - 256; }
+// the most dynamic LDS a streamed flow2 launch may take (sw_flow2.hip flow2_dyn_lds): the staged
+// limit less the 4 per-wave code rings (F2_CR = 256 rows + a chunk + 64 sinks each)
+__host__ __device__ constexpr int flow2_stream_dyn_max(int C) { return flow2_stage_max(C) - 4 * (256 + C + 64); }
 // flow2 pair per workgroup (LaunchCfg::f2_pwg): the wave 3 -> wave 0 buffer holds a round's
 // rows (int2 each) in the dynamic LDS; workgroups per CU that fit beside the static LDS
 // (4 rings) and the 4 streamed code rings

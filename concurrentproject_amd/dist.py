@@ -110,17 +110,26 @@ class ColumnSlabs:
     def columns(self) -> tuple:
         return self.bounds[self.rank], self.bounds[self.rank + 1]
 
-    def run(self, d_arena_ptr: int, col_off: int, row_off: int, stream: Optional[int] = None) -> torch.Tensor:
-        """Score this rank's slab of the pair whose columns start at byte col_off and
-        rows at row_off of the device arena; returns the pair's score (1-int tensor,
-        identical on every rank).  Asynchronous on `stream` (torch's current stream)."""
+    def launch(self, d_arena_ptr: int, col_off: int, row_off: int, stream: Optional[int] = None) -> None:
+        """Enqueue this rank's slab kernel (a fresh epoch) on `stream`; self.score then holds
+        the slab's max.  The pair whose columns start at byte col_off and rows at row_off
+        of the device arena."""
         from . import score_slab_device
         self.epoch += 1
         lo, hi = self.columns
         score_slab_device(d_arena_ptr, col_off + lo, hi - lo, row_off, self.m,
                           self.inflow.ptr if self.inflow else 0, self.outflow, self.epoch,
                           self.score.data_ptr(), self.flags, stream)
+
+    def reduce(self) -> torch.Tensor:
+        """The pair's score: all-reduce(MAX) of the slab maxima (1-int tensor, identical on
+        every rank).  It also orders launches: rank r's next kernel is queued behind it."""
         return slab_max(self.score, self.group)
+
+    def run(self, d_arena_ptr: int, col_off: int, row_off: int, stream: Optional[int] = None) -> torch.Tensor:
+        """launch + reduce: score this rank's slab and return the pair's score."""
+        self.launch(d_arena_ptr, col_off, row_off, stream)
+        return self.reduce()
 
     def close(self) -> None:
         from . import ipc_close

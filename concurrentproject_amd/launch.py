@@ -44,15 +44,85 @@ def rank_env(environ=None) -> tuple:
 
 
 def visible_devices() -> int:
-    """GPUs this process could use.  torch.cuda.device_count() does not initialise
-    HIP on this image, so the parent stays clean for spawning."""
+    """GPUs this rank can use (HIP's count; a rank may initialise HIP).  The parent of
+    spawned ranks counts with gpu_count() instead, which makes no HIP call at all."""
     import torch
     return int(torch.cuda.device_count())
 
 
+KFD_TOPOLOGY = "/sys/class/kfd/kfd/topology/nodes"
+
+
+def _props(path: str) -> dict:
+    out = {}
+    with open(path) as f:
+        for line in f:
+            parts = line.split()
+            if len(parts) == 2:
+                out[parts[0]] = parts[1]
+    return out
+
+
+def kfd_gpus(root: Optional[str] = None, dri: Optional[str] = None) -> list:
+    """The GPU agents ROCr would enumerate, read from the KFD topology without any HIP or
+    driver call: nodes with SIMDs (CPU nodes have none) whose render node
+    /dev/dri/renderD<drm_render_minor> this process may open, in node order.  Each entry
+    is the node's properties.  Raises LaunchError if the topology cannot be read."""
+    root = root or os.environ.get("SW_KFD_TOPOLOGY", KFD_TOPOLOGY)
+    dri = dri or os.environ.get("SW_DRI_DIR", "/dev/dri")
+    try:
+        nodes = sorted((int(d) for d in os.listdir(root) if d.isdigit()))
+    except OSError as e:
+        raise LaunchError("cannot count GPUs: KFD topology %s unreadable (%s)" % (root, e)) from None
+    gpus = []
+    for k in nodes:
+        try:
+            pr = _props(os.path.join(root, str(k), "properties"))
+        except OSError:
+            continue
+        if int(pr.get("simd_count", "0")) <= 0:
+            continue
+        node = os.path.join(dri, "renderD%s" % pr.get("drm_render_minor", "-1"))
+        if not os.access(node, os.R_OK | os.W_OK):
+            continue
+        gpus.append(pr)
+    return gpus
+
+
+def gpu_count(environ=None, root: Optional[str] = None, dri: Optional[str] = None) -> int:
+    """Visible GPUs without initialising HIP: the KFD GPUs (kfd_gpus), narrowed by
+    ROCR_VISIBLE_DEVICES (indices or GPU-<hex unique id>) and then by HIP_VISIBLE_DEVICES
+    (or CUDA_VISIBLE_DEVICES): indices into that list, counted up to the first invalid one."""
+    env = os.environ if environ is None else environ
+    gpus = kfd_gpus(root, dri)
+    rocr = env.get("ROCR_VISIBLE_DEVICES")
+    if rocr is not None:
+        ids = {"GPU-%x" % int(g.get("unique_id", "0")): g for g in gpus}
+        keep = []
+        for tok in [t.strip() for t in rocr.split(",") if t.strip()]:
+            if tok.isdigit() and int(tok) < len(gpus):
+                keep.append(gpus[int(tok)])
+            elif tok.lower() in {k.lower() for k in ids}:
+                keep.append(next(v for k, v in ids.items() if k.lower() == tok.lower()))
+            else:
+                break
+        gpus = keep
+    n = len(gpus)
+    hip = env.get("HIP_VISIBLE_DEVICES", env.get("CUDA_VISIBLE_DEVICES"))
+    if hip is not None:
+        count = 0
+        for tok in [t.strip() for t in hip.split(",") if t.strip()]:
+            if not tok.isdigit() or int(tok) >= n:
+                break
+            count += 1
+        n = count
+    return n
+
+
 def require_devices(n: int, devices: Optional[int] = None) -> int:
-    """Raise LaunchError unless at least n GPUs are visible; returns the count."""
-    have = visible_devices() if devices is None else devices
+    """Raise LaunchError unless at least n GPUs are visible; returns the count.  The count
+    is gpu_count()'s (KFD topology, no HIP call): this runs in the parent of the ranks."""
+    have = gpu_count() if devices is None else devices
     if have < n:
         raise LaunchError("--gpus %d needs %d visible GPUs, this host shows %d "
                           "(HIP_VISIBLE_DEVICES=%r)" % (n, n, have, os.environ.get("HIP_VISIBLE_DEVICES")))

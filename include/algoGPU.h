@@ -68,6 +68,20 @@ int sw_score_batch(const unsigned char* const* a, const int* alen,
                    const unsigned char* const* b, const int* blen,
                    int npairs, int* scores_out);
 
+/* The same batch over the first ngpus visible GPUs of the node (SURVEY.md 8(b), configs
+ * C3/C4): pairs are cut into contiguous shards (sw_batch_shard: sizes differ by at most
+ * one), each scored by its own host thread and stream on its own device, and the int32
+ * scores of devices 1..ngpus-1 are gathered to device 0 over RCCL (ncclSend/ncclRecv in
+ * one group; RCCL is loaded at the first call with ngpus > 1) -- the only exchange, no
+ * data-path collective.  Synchronous like the reference ABI; scores_out in pair order.
+ * Returns 0, or -1 with sw_last_error() (e.g. ngpus above the visible devices).
+ * Callers: the reference harness's batched loops (TestFileWithGPU.cpp:82-94). */
+int sw_score_batch_multi(const unsigned char* const* a, const int* alen,
+                         const unsigned char* const* b, const int* blen,
+                         int npairs, int* scores_out, int ngpus);
+/* Shard [*lo, *hi) of rank `rank` of ngpus for npairs pairs (no GPU call).  0 or -1. */
+int sw_batch_shard(int npairs, int ngpus, int rank, int* lo, int* hi);
+
 /* Batch whose sequences are already resident in device memory (one arena,
  * byte offsets per sequence).  Offsets/lengths are HOST arrays; d_scores is a
  * device array of npairs ints.  Asynchronous on `stream` (a hipStream_t; NULL =
@@ -104,7 +118,9 @@ int sw_stream_status(void* stream);
  *   Asynchronous on `stream` as sw_score_batch_device.
  * sw_slab_alloc: a zeroed inflow buffer of m granules; returns 1 (fine-grained
  *   memory) or 2 (device memory), -1 on error; ipc_handle (SW_IPC_HANDLE_BYTES,
- *   may be NULL) receives its hipIpcMemHandle_t for the writing rank.
+ *   may be NULL) receives its hipIpcMemHandle_t for the writing rank.  An exported
+ *   buffer (ipc_handle != NULL: the edge another GPU writes) must be fine-grained:
+ *   without it the call fails (-1) unless option "slab_plain" is 1.
  * sw_ipc_open / sw_ipc_close: map / unmap another process's buffer. */
 #define SW_IPC_HANDLE_BYTES 64
 int sw_slab_bounds(long long n, int m, int nslabs, int flags, long long* bounds);
@@ -173,6 +189,10 @@ void sw_db_close(sw_db* db);
  *   "f2pwg"    DNA batches whose scores need int32 (no 16-bit duos): -1 = (default) the
  *              flow2 step with a pair per workgroup when its constants fit, 0 = never
  *              (the pair-per-workgroup strip kernel), 1 = also for a forced mode 5 batch
+ *   "f3"       1 = (default) a staged two-column linear-gap flow2 launch (C = 32: C2) runs the
+ *              flow3 kernel (hand-scheduled chunk loops), 0 = the compiled flow2 kernel
+ *   "slab_plain" 1 = an exported slab buffer may fall back to plain device memory (one-GPU
+ *              tests only; cross-GPU edges need fine-grained memory), 0 = (default) refuse
  *   "trace"    device address of a 16 x u64 per-strip trace buffer, 0 = off (tools)
  * Returns 0, or -1 for an unknown key / bad value. */
 int sw_set_option(const char* key, long long value);
@@ -188,7 +208,8 @@ typedef struct {
     int mode;
     int variant;            /* bit 0: duo max3 via v_pk_maximum3_f16; bit 1: flow2 streams row codes;
                                bit 2: flow2 ring edges; bit 3: the linear-gap step;
-                               bit 4: flow2 two columns per lane; bit 5: flow2 pair per workgroup */
+                               bit 4: flow2 two columns per lane; bit 5: flow2 pair per workgroup;
+                               bit 6: the flow3 kernel (sw_flow3.hip) */
 } sw_stats;
 int sw_last_stats(sw_stats* out);
 

@@ -32,38 +32,27 @@ def main():
     import torch.distributed as dist
     dist.init_process_group("gloo")          # env:// from the launcher's variables
     try:
+        import bench   # the rank logic bench.py runs at N GPUs, with the oracle as the scorer
         import oracle
-        from concurrentproject_amd.dist import gather_scores, shard_bounds, slab_max
         res = {"world": dist.get_world_size(), "rank_env": [world, rank, local]}
         if mode == "batch":
             n, per = int(sys.argv[3]), int(sys.argv[4])
-            lo, hi = shard_bounds(per * world, world, rank)
-            local_scores = torch.tensor([oracle.score_linear(*oracle.gen_pair(8192 + k, n)) for k in range(lo, hi)],
-                                        dtype=torch.int32)
-            full = gather_scores(local_scores, per * world)
-            res["scores"] = None if full is None else full.tolist()
+            job = bench.BatchRank(torch, dist, world, rank, n, per, scorer="oracle")
+            t_max, kern_ms = bench.time_launches(torch, job.launch, job.collective, 1, 0, job.stream, dist)
+            res["scores"] = job.result()
+            res["shard"] = [job.lo, job.hi]
         elif mode == "slab":
-            import concurrentproject_amd as sw
             n, m = int(sys.argv[3]), int(sys.argv[4])
             a, b = oracle.gen_pair(1048576, n)
-            b = b[:m]
-            bounds = sw.slab_bounds(n, m, world, sw.SW_FLAG_DNA)
-            lo, hi = bounds[rank], bounds[rank + 1]
-            edge = None
-            if rank > 0:
-                eh = torch.empty(m, dtype=torch.int32)
-                ee = torch.empty(m, dtype=torch.int32)
-                dist.recv(eh, src=rank - 1)
-                dist.recv(ee, src=rank - 1)
-                edge = (eh.numpy(), ee.numpy())
-            best, (oh, oe) = oracle.slab(a[lo:hi], b, edge=edge)
-            if rank + 1 < world:
-                dist.send(torch.from_numpy(np.ascontiguousarray(oh)), dst=rank + 1)
-                dist.send(torch.from_numpy(np.ascontiguousarray(oe)), dst=rank + 1)
-            score = slab_max(torch.tensor([best], dtype=torch.int32))
+            job = bench.SlabRank(torch, dist, n, m, a, b[:m], scorer="oracle")
+            t_max, kern_ms = bench.time_launches(torch, job.launch, job.collective, 2, 0, job.stream, dist)
+            score = torch.tensor([job.result()], dtype=torch.int32)
             allsc = [torch.zeros(1, dtype=torch.int32) for _ in range(world)]
             dist.all_gather(allsc, score)
-            res.update(score=int(score.item()), every_rank=[int(x.item()) for x in allsc], bounds=bounds)
+            rep = job.report(kern_ms)
+            res.update(score=int(score.item()), every_rank=[int(x.item()) for x in allsc], bounds=job.slabs.bounds,
+                       report=rep)
+            job.close()
         if rank == 0:
             with open(out, "w") as f:
                 json.dump(res, f)

@@ -41,6 +41,7 @@ def test_launcher_batch_gloo_matches_c4_golden(tmp_path):
     gold = json.load(open(os.path.join(ROOT, "tests", "golden", "configs.json")))
     ref = gold.get("C4", gold["C3"])["scores"]
     assert res["scores"] == ref[:4]
+    assert res["shard"] == [0, 2]
 
 
 @pytest.mark.parametrize("world,n,m", [(2, 1500, 700), (3, 1000, 450)])
@@ -56,6 +57,9 @@ def test_launcher_slab_gloo(tmp_path, world, n, m):
     exp = oracle.score_linear(a, b[:m])
     assert res["score"] == exp and res["every_rank"] == [exp] * world
     assert len(set(res["bounds"])) == world + 1
+    rep = res["report"]   # bench.py's slab_ranks record, built by the same SlabRank.report
+    assert rep["per_rank_columns"] == [res["bounds"][r + 1] - res["bounds"][r] for r in range(world)]
+    assert rep["inflow_fine_grained"] == [None] * world and len(rep["per_rank_kernel_ms"]) == world
 
 
 def test_launcher_failure_stops_the_job(tmp_path):
@@ -76,7 +80,7 @@ def test_bench_refuses_more_gpus_than_visible():
                        capture_output=True, text=True, timeout=300,
                        env={k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "TORCHELASTIC_RUN_ID")})
     assert p.returncode == 2, (p.returncode, p.stderr[-2000:])
-    assert "needs 2 visible GPUs" in p.stderr
+    assert "needs 2 visible GPUs" in p.stderr or "cannot count GPUs" in p.stderr
     assert p.stdout.strip() == ""
 
 
@@ -87,3 +91,71 @@ def test_bench_gpus_must_match_launcher_world():
                        capture_output=True, text=True, timeout=300, env=env)
     assert p.returncode != 0
     assert "launcher started 1 ranks" in p.stderr
+
+
+def _fake_topology(tmp_path, ngpu, ncpu=2, unreadable=()):
+    """A KFD topology with ncpu CPU nodes and ngpu GPU nodes, and their render nodes."""
+    topo, dri = tmp_path / "nodes", tmp_path / "dri"
+    topo.mkdir()
+    dri.mkdir()
+    k = 0
+    for _ in range(ncpu):
+        (topo / str(k)).mkdir()
+        (topo / str(k) / "properties").write_text("cpu_cores_count 64\nsimd_count 0\ndrm_render_minor 0\n")
+        k += 1
+    for g in range(ngpu):
+        (topo / str(k)).mkdir()
+        (topo / str(k) / "properties").write_text(
+            "cpu_cores_count 0\nsimd_count 1024\ndrm_render_minor %d\nunique_id %d\n" % (128 + g, 1000 + g))
+        if g not in unreadable:
+            (dri / ("renderD%d" % (128 + g))).write_text("")
+        k += 1
+    return str(topo), str(dri)
+
+
+def test_gpu_count_from_kfd_topology(tmp_path):
+    """The parent of the ranks counts GPUs from the KFD topology (no HIP call), narrowed
+    by the visibility variables; a render node it cannot open does not count."""
+    from concurrentproject_amd.launch import LaunchError, gpu_count
+    topo, dri = _fake_topology(tmp_path, 8, unreadable=(5,))
+    assert gpu_count({}, topo, dri) == 7
+    assert gpu_count({"HIP_VISIBLE_DEVICES": "0,1,2"}, topo, dri) == 3
+    assert gpu_count({"CUDA_VISIBLE_DEVICES": "1"}, topo, dri) == 1
+    assert gpu_count({"HIP_VISIBLE_DEVICES": "0,9,1"}, topo, dri) == 1     # stops at the first invalid index
+    assert gpu_count({"HIP_VISIBLE_DEVICES": ""}, topo, dri) == 0
+    assert gpu_count({"ROCR_VISIBLE_DEVICES": "2,3", "HIP_VISIBLE_DEVICES": "1"}, topo, dri) == 1
+    assert gpu_count({"ROCR_VISIBLE_DEVICES": "GPU-%x" % 1003}, topo, dri) == 1
+    with pytest.raises(LaunchError, match="cannot count GPUs"):
+        gpu_count({}, str(tmp_path / "missing"), dri)
+
+
+def test_bench_parent_never_initialises_hip(tmp_path, monkeypatch):
+    """`bench.py --gpus 2`: the parent reaches spawn_ranks with HIP's device count made to
+    raise (so it cannot have called it), and exits 2 when the topology shows too few GPUs."""
+    import torch
+    import bench
+    import concurrentproject_amd.launch as launch
+
+    def no_hip(*a, **k):
+        raise AssertionError("the parent of the ranks called HIP")
+    monkeypatch.setattr(torch._C, "_cuda_getDeviceCount", no_hip, raising=False)
+    monkeypatch.setattr(torch.cuda, "device_count", no_hip)
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    monkeypatch.delenv("TORCHELASTIC_RUN_ID", raising=False)
+    monkeypatch.delenv("HIP_VISIBLE_DEVICES", raising=False)
+    monkeypatch.delenv("CUDA_VISIBLE_DEVICES", raising=False)
+    monkeypatch.delenv("ROCR_VISIBLE_DEVICES", raising=False)
+    calls = []
+    monkeypatch.setattr(launch, "spawn_ranks", lambda n, argv, **kw: calls.append((n, argv)) or 0)
+    topo, dri = _fake_topology(tmp_path, 2)
+    monkeypatch.setenv("SW_KFD_TOPOLOGY", topo)
+    monkeypatch.setenv("SW_DRI_DIR", dri)
+
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "2", "--steps", "1"])
+    assert bench.start_ranks(bench.parse()) == 0
+    assert calls and calls[0][0] == 2 and calls[0][1][1].endswith("bench.py")
+    topo1, dri1 = _fake_topology(tmp_path / "one", 1) if (tmp_path / "one").mkdir() is None else (None, None)
+    monkeypatch.setenv("SW_KFD_TOPOLOGY", topo1)
+    monkeypatch.setenv("SW_DRI_DIR", dri1)
+    assert bench.start_ranks(bench.parse()) == 2
+    assert len(calls) == 1

@@ -281,4 +281,7 @@ def test_slabs_two_processes_ipc(oracle_mod, stream_codes):
     for rank, got, bounds, fine, err in res:
         assert err is None, (rank, err)
         assert got == [exp, exp], (rank, got, exp, bounds)
+    # rank 1's inflow is exported for rank 0's kernel: fine-grained memory (sw_slab_alloc
+    # refuses plain memory for an exported buffer), rank 0 has no inflow
+    assert res[0][3] is None and res[1][3] is True, res
     print("slab IPC: bounds", res[0][2], "rank-1 inflow fine-grained:", res[1][3])
