@@ -36,7 +36,7 @@ def test_multi_one_gpu_c3_golden(engine, golden):
     assert engine.score_batch(pairs, ngpus=1) == c["scores"]
     assert engine.last_stats()["cells"] == c["npairs"] * N * N
     # ragged and empty pairs keep their slots
-    mixed = [pairs[0], (b"", b"ACGT"), pairs[1][:1], (b"ACGTACGT", b"ACG"), pairs[2]]
+    mixed = [pairs[0], (b"", b"ACGT"), (pairs[1][0][:1], pairs[1][1]), (b"ACGTACGT", b"ACG"), pairs[2]]
     assert engine.score_batch(mixed, ngpus=1) == engine.score_batch(mixed)
 
 
@@ -47,4 +47,4 @@ def test_multi_more_gpus_than_visible(engine):
     with pytest.raises(engine.SwError, match="visible"):
         engine.score_batch([(b"ACGT", b"ACGT")], ngpus=n + 1)
     with pytest.raises(engine.SwError, match="visible"):
-        engine.score_batch([(b"ACGT", b"ACGT")], n + 7)
+        engine.score_batch([(b"ACGT", b"ACGT")], ngpus=n + 7)
