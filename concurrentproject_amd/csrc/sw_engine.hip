@@ -351,8 +351,11 @@ bool flow2_staged(const Job& job, int max_m) {
 // of 5.5 VALU per 64 cells, throughput-bound).
 bool flow2_w2_wanted(const Job& job, const Params& p) {
     const long long o = g_opt_f2w.load();
-    const bool lin = p.gap_init == p.gap_ext && g_opt_linear.load() != 0 && job.C != 16 &&
-                     (g_opt_C.load() == 0 || g_opt_C.load() == 32 || g_opt_C.load() == 64);
+    // (C = 16: flow3's staged kernel only, sw_flow3.hip; flow2 has no such two-column variant)
+    const bool c16 = g_opt_f3.load() != 0;
+    const bool lin = p.gap_init == p.gap_ext && g_opt_linear.load() != 0 && (job.C != 16 || c16) &&
+                     (g_opt_C.load() == 0 || g_opt_C.load() == 32 || g_opt_C.load() == 64 ||
+                      (g_opt_C.load() == 16 && c16));
     return lin && o != 1;
 }
 
@@ -636,9 +639,18 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
     // G_INIT == G_EXT: the exact linear-gap step (sw_flow2.hip LIN), unless disabled; the
     // pair-per-workgroup kernel is built with it exactly at two columns per lane
     const bool f2_lin = job.pwg ? job.f2w2
-                                : ((job.mode == MODE_FLOW2 && (job.C == 32 || job.C == 64)) ||
+                                : ((job.mode == MODE_FLOW2 &&
+                                    (job.C == 32 || job.C == 64 || (job.C == 16 && job.f2w2))) ||
                                    (job.mode == MODE_DUO && job.duo_f16)) &&
                                       prm.gap_init == prm.gap_ext && g_opt_linear.load() != 0;
+    // flow3 (sw_flow3.hip, hand-scheduled chunk loops) for the two-column linear-gap launches it
+    // implements: the staged single-pair kernel (C = 32, rows in LDS: C2) and ring mode (C = 64,
+    // streamed rows, one pair: C5); option f3 = 0 keeps flow2
+    int max_m_f3 = 0;
+    for (const PairDesc& d : job.pairs) max_m_f3 = std::max(max_m_f3, d.m);
+    const bool f3_base = g_opt_f3.load() != 0 && job.mode == MODE_FLOW2 && job.f2w2 && f2_lin && !job.pwg;
+    const bool use_f3 = f3_base && ((!f2s && !job.ring && flow3_fits(max_m_f3, job.C)) ||
+                                    (job.ring && edge == nullptr && job.C == 64));
     // read once: it sizes the ring arena here and addresses it in the kernel (kp.ring_rows)
     const long long ring_rows = g_opt_ring_rows.load();
     int ring_blocks = 0, wrap_rows = 0;
@@ -653,7 +665,7 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
         int fit = 0;
         for (;; --f2_wgs) {
             probe.f2_wgs = f2_wgs;
-            fit = flow2_stream_resident(probe, true, edge != nullptr);
+            fit = use_f3 ? flow3_ring_resident(probe) : flow2_stream_resident(probe, true, edge != nullptr);
             if (fit >= f2_wgs || f2_wgs == 1) break;
         }
         if (fit < 1) {
@@ -715,8 +727,11 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
     cfg.f2_pwg = job.mode == MODE_FLOW2 && job.pwg;
     // the staged two-column linear-gap kernel with hand-scheduled chunk loops (sw_flow3.hip), unless
     // option f3 = 0: C2
-    cfg.f3 = g_opt_f3.load() != 0 && cfg.f2_w2 && f2_lin && !f2s && !cfg.f2_pwg && !job.ring && job.C == 32 &&
-             flow3_fits(max_m);
+    cfg.f3 = use_f3;
+    if (cfg.f2_w2 && job.C == 16 && !use_f3) {
+        set_err("flow2: two columns per lane at C = 16 runs on flow3 only (rows staged in LDS, one GPU)");
+        return -1;
+    }
     if (cfg.f2_w2 && !f2_lin) {   // the strips were cut for two columns per lane
         set_err("flow2: two columns per lane needs the linear-gap step");
         return -1;

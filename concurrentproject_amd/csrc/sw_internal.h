@@ -181,7 +181,9 @@ hipError_t raise_dyn_lds(const void* fn, int bytes);
 hipError_t launch_sw_flow2(const LaunchCfg& cfg, const KParams& kp, hipStream_t stream);
 // flow3 (sw_flow3.hip): flow2's staged W2 linear-gap kernel with hand-scheduled chunk loops
 hipError_t launch_sw_flow3(const LaunchCfg& cfg, const KParams& kp, hipStream_t stream);
-bool flow3_fits(int max_m);
+bool flow3_fits(int max_m, int C);
+// workgroups per CU resident for a flow3 ring-mode launch (its LDS pad of cfg.f2_wgs), -1 on error
+int flow3_ring_resident(const LaunchCfg& cfg);
 int flow2_waves_per_cu(int C);
 // workgroups per CU resident for the streamed flow2 kernel cfg selects (ring / slab
 // instantiation, LDS pad of cfg.f2_wgs); -1 on error (sw_flow2.hip)

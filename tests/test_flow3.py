@@ -57,20 +57,23 @@ def test_flow3_ragged(engine, oracle_mod):
     engine.set_option("orient", 1)
     engine.set_option("mode", 5)      # flow2 planning for every shape (single strips included)
     engine.set_option("f2w", 2)
-    for prm in (engine.Params(), engine.Params(2, -3, 4, 4), engine.Params(1, 0, 0, 0)):
-        op = oracle_mod.Params(prm.match, prm.mismatch, prm.gap_init, prm.gap_ext)
-        exp = [oracle_mod.score_linear(a, b, op) for a, b in pairs]
-        got = []
-        for a, b in pairs:
-            got.append(engine.score(a, b, prm))
-            st = engine.last_stats()
-            assert st["mode"] == 5 and st["variant"] & 64 and st["variant"] & 16, st
-        assert got == exp, prm
-        assert engine.score_batch(pairs, prm) == exp, prm
-        for blocks in (1, 2, 3):
-            engine.set_option("blocks", blocks)
-            assert engine.score_batch(pairs, prm) == exp, (prm, blocks)
-        engine.set_option("blocks", 0)
+    for C in (32, 16):   # 32-row chunks (automatic) and 16 (option C)
+        engine.set_option("C", C)
+        for prm in (engine.Params(), engine.Params(2, -3, 4, 4), engine.Params(1, 0, 0, 0)):
+            op = oracle_mod.Params(prm.match, prm.mismatch, prm.gap_init, prm.gap_ext)
+            exp = [oracle_mod.score_linear(a, b, op) for a, b in pairs]
+            got = []
+            for a, b in pairs:
+                got.append(engine.score(a, b, prm))
+                st = engine.last_stats()
+                assert st["mode"] == 5 and st["variant"] & 64 and st["variant"] & 16 and st["C"] == C, st
+            assert got == exp, (prm, C)
+            assert engine.score_batch(pairs, prm) == exp, (prm, C)
+            for blocks in (1, 2, 3):
+                engine.set_option("blocks", blocks)
+                assert engine.score_batch(pairs, prm) == exp, (prm, blocks, C)
+            engine.set_option("blocks", 0)
+    engine.set_option("C", 0)
 
 
 def test_flow3_matches_flow2(engine):
@@ -120,3 +123,63 @@ def test_flow3_config_c2(engine, golden):
         st = engine.last_stats()
         assert st["mode"] == 5 and st["variant"] & 64 and not st["variant"] & 2, st
         assert score.item() == c["score"]
+
+
+# ---- ring mode (sw_flow3.hip sw_flow3r_kernel: streamed row codes, group edges through
+# per-block rings, C = 64; the C5 organisation)
+
+def _ring_opts(engine, blocks, rows):
+    engine.set_option("ring", 1)
+    engine.set_option("blocks", blocks)
+    engine.set_option("ring_rows", rows)
+
+
+@pytest.fixture
+def _ring_reset(engine):
+    yield
+    engine.set_option("ring", -1)
+    engine.set_option("ring_rows", 4096)
+    engine.set_option("blocks", 0)
+
+
+def test_flow3_ring_parity(engine, oracle_mod, _ring_reset):
+    """Ring mode forced on grids of 1, 2, 3 and 7 blocks with 512-row rings (many rounds,
+    the wrap ring every round), rows around the 64-row chunk pairs, three constant sets."""
+    rng = np.random.default_rng(34)
+    pairs = _pairs(rng, [(253, 700), (1009, 513), (2017, 3001), (4096, 2600), (5000, 1200), (9000, 2000),
+                         (3025, 127), (2521, 129)])
+    engine.set_option("orient", 1)
+    for prm in (engine.Params(), engine.Params(2, -3, 4, 4), engine.Params(1, 0, 0, 0)):
+        op = oracle_mod.Params(prm.match, prm.mismatch, prm.gap_init, prm.gap_ext)
+        exp = [oracle_mod.score_linear(a, b, op) for a, b in pairs]
+        for blocks, rows in ((0, 4096), (1, 512), (2, 512), (3, 1024), (7, 512)):
+            _ring_opts(engine, blocks, rows)
+            got = []
+            for a, b in pairs:
+                got.append(engine.score(a, b, prm))
+                st = engine.last_stats()
+                groups = (((len(a) - 2 + 125) // 126 if len(a) > 128 else 1) + 3) // 4
+                if groups > 1:
+                    assert st["variant"] & 64 and st["variant"] & 4 and st["C"] == 64, st
+            assert got == exp, (prm, blocks, rows)
+
+
+def test_flow3_ring_matches_flow2(engine, _ring_reset):
+    """A 2^17 pair in ring mode (520 groups) on flow3 and on flow2 (f3 = 0): the same score."""
+    import torch
+    N = 1 << 17
+    a, b = engine.gen_pair(N, N)
+    arena = torch.from_numpy(np.concatenate([a, b])).cuda()
+    score = torch.full((1,), -1, dtype=torch.int32, device="cuda")
+    s = torch.cuda.current_stream()
+    engine.set_option("ring", 1)
+    out = []
+    for f3 in (1, 0):
+        engine.set_option("f3", f3)
+        engine.score_batch_device(arena.data_ptr(), [0], [N], [N], [N], score.data_ptr(), flags=1,
+                                  stream=s.cuda_stream)
+        engine.stream_status(s.cuda_stream)
+        st = engine.last_stats()
+        assert bool(st["variant"] & 64) == bool(f3) and st["variant"] & 4, st
+        out.append(score.item())
+    assert out[0] == out[1] > 0

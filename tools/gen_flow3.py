@@ -45,37 +45,50 @@ ROLES_IN = ("none", "lds")
 ROLES_OUT = ("none", "lds", "gran")
 
 
-def step(a, io, l0, b):
+# step registers of the staged (C2) loops: H_A, max(H_A - G, 0), H_B, max(H_B - G, 0), tA, tB,
+# the score bytes of columns A / B for 4 rows, the running max
+STAGED = dict(H="v66", HGO="v67", HB="v68", HGOB="v69", TA="v70", TB="v71", PA="v72", PB="v73", M="v74")
+
+
+def step(a, io, l0, b, r=STAGED):
     """One anti-diagonal step of the two-column linear-gap step (9 VALU, 128 cells)."""
-    a(f"v_add_u32_sdwa v70, sext(v72), {l0} dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_{b} src1_sel:DWORD")
-    a(f"v_add_u32_sdwa v71, sext(v73), v66 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_{b} src1_sel:DWORD")
+    a(f"v_add_u32_sdwa {r['TA']}, sext({r['PA']}), {l0} dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_{b} "
+      "src1_sel:DWORD")
+    a(f"v_add_u32_sdwa {r['TB']}, sext({r['PB']}), {r['H']} dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_{b} "
+      "src1_sel:DWORD")
     a(f"v_mov_b32_dpp {l0}, {io} wave_shl:1 row_mask:0xf bank_mask:0xf")
-    a(f"v_add_u32_dpp {io}, v68, %[ng] wave_shr:1 row_mask:0xf bank_mask:0xf")
-    a(f"v_max3_i32 v66, {io}, v67, v70")
-    a("v_sub_u32_e64 v67, v66, %[G] clamp")
-    a("v_max3_i32 v68, v67, v69, v71")
-    a("v_sub_u32_e64 v69, v68, %[G] clamp")
-    a("v_max3_i32 v74, v74, v70, v71")
+    a(f"v_add_u32_dpp {io}, {r['HB']}, %[ng] wave_shr:1 row_mask:0xf bank_mask:0xf")
+    a(f"v_max3_i32 {r['H']}, {io}, {r['HGO']}, {r['TA']}")
+    a(f"v_sub_u32_e64 {r['HGO']}, {r['H']}, %[G] clamp")
+    a(f"v_max3_i32 {r['HB']}, {r['HGO']}, {r['HGOB']}, {r['TB']}")
+    a(f"v_sub_u32_e64 {r['HGOB']}, {r['HB']}, %[G] clamp")
+    a(f"v_max3_i32 {r['M']}, {r['M']}, {r['TA']}, {r['TB']}")
 
 
-def granule(a):
-    """Publish the 16 newest outflow rows (lanes 48..63 of the IO register v64) as
-    8-B granules {H-G, (H-G) ^ epoch ^ 0x5BD1E995} at row * 8 of the group edge,
-    write-through (sw_flow3.hip header).  v105 = this lane's row * 8 (rows < 0
-    wrap to huge offsets: dropped by the buffer range check, as are rows past 2m)."""
+def granule(a, rows):
+    """Publish the `rows` newest outflow rows (lanes 64-rows..63 of the IO register v64,
+    mask %[m48]) as 8-B granules {H-G, (H-G) ^ epoch ^ 0x5BD1E995} at row * 8 of the group
+    edge, write-through (sw_flow3.hip header).  v105 = this lane's row * 8 (rows < 0 wrap
+    to huge offsets: dropped by the buffer range check, as are rows past 2m)."""
     a("v_mov_b32 v100, v64")
     a("v_xor_b32 v101, %[ek], v64")
     a("v_cndmask_b32_e64 v106, -16, v105, %[m48]")
-    a("v_add_u32 v105, 0x80, v105")     # (an independent VALU between the data writes and the store)
+    a(f"v_add_u32 v105, {rows * 8:#x}, v105")    # (an independent VALU between the data writes and the store)
     a("buffer_store_dwordx2 v[100:101], v106, %[rsrc], 0 offen sc1")
 
 
-def gen_role(IN, OUT_, spec=0, halfpub=True):
+def gen_role(IN, OUT_, spec=0, halfpub=True, C=32):
+    """The staged loop of one strip role at C-row chunks (C = 32 or 16)."""
     L = []
     a = L.append
     lds_in, lds_out, gran = IN == "lds", OUT_ == "lds", OUT_ == "gran"
+    nd = C // 4                         # row-code dwords per chunk
+    ncr = nd // 4                       # their 16-B LDS reads
     nw = 3 if lds_out else 0            # LDS writes of a chunk's publish
-    # ---- entry
+    grows = C // 2 if halfpub else C    # rows per granule publish
+    # ---- entry (s_nop 4: the "s" operands may be fresh from v_readfirstlane, and buffer
+    # instructions read them as descriptors: 5 wait states)
+    a("s_nop 4")
     a("s_waitcnt vmcnt(0) lgkmcnt(0)")
     for r in ("v66", "v67", "v68", "v69", "v74"):
         a(f"v_mov_b32 {r}, 0")
@@ -83,20 +96,20 @@ def gen_role(IN, OUT_, spec=0, halfpub=True):
     a("v_mov_b32 v65, %[ng]")
     a("v_mov_b32 v94, %[code]")
     a("s_mov_b32 s40, 0")
-    a("s_movk_i32 s41, 0x80")           # ((k0 + 32) mod R) * 4 at k0 = 0
+    a(f"s_movk_i32 s41, {(64 - C) * 4:#x}")       # ((k0 + 64 - C) mod R) * 4 at k0 = 0
     a("s_mov_b32 s45, 0")
     a("s_mov_b32 s46, 0")
     a(f"s_movk_i32 s44, {R}")            # consumer word seen: 0 rows consumed (+ R)
     if lds_out:
-        a("v_mov_b32 v97, -96")          # producer word at chunk 0: k0 - 64 rows out, minus 32
+        a(f"v_mov_b32 v97, {-64 - C}")   # producer word at chunk 0: k0 - 64 rows out, minus C
         a("v_add_u32 v96, s41, %[lout]")
     if lds_in:
-        a(f"v_mov_b32 v98, {R + 32}")    # consumer word after chunk 0: 32 rows consumed (+ R)
+        a(f"v_mov_b32 v98, {R + C}")     # consumer word after chunk 0: C rows consumed (+ R)
         a("v_add_u32 v95, s41, %[lin]")
     if gran:
         a("v_mov_b32 v105, %[lrow]")
-    a("ds_read_b128 v[76:79], v94")
-    a("ds_read_b128 v[80:83], v94 offset:16")
+    for q in range(ncr):
+        a(f"ds_read_b128 v[{76 + 4 * q}:{79 + 4 * q}], v94 offset:{16 * q}")
     if lds_in and spec:
         a("ds_read_b32 v93, %[pin]")
         a("ds_read_b32 v92, v95")
@@ -104,7 +117,7 @@ def gen_role(IN, OUT_, spec=0, halfpub=True):
     for p in (0, 1):
         cur = 76 if p == 0 else 84
         nxt = 84 if p == 0 else 76
-        o0, o1 = (32, 48) if p == 0 else (64, 80)
+        obase = C if p == 0 else 2 * C
         # ---- chunk top: publish the last chunk's outflow, take this chunk's inflow
         if lds_in and not spec:
             a("ds_read_b32 v93, %[pin]")
@@ -118,11 +131,11 @@ def gen_role(IN, OUT_, spec=0, halfpub=True):
             a(f"ds_write_b32 v96, v64 offset:{R * 4}")
             a("ds_write_b32 %[pout], v97")
         if gran:
-            granule(a)
-        a(f"ds_read_b128 v[{nxt}:{nxt + 3}], v94 offset:{o0}")
-        a(f"ds_read_b128 v[{nxt + 4}:{nxt + 7}], v94 offset:{o1}")
+            granule(a, grows)
+        for q in range(ncr):
+            a(f"ds_read_b128 v[{nxt + 4 * q}:{nxt + 4 * q + 3}], v94 offset:{obase + 16 * q}")
         if lds_in:
-            after = 1 + nw + 2           # LDS ops issued after the producer-word read
+            after = 1 + nw + ncr         # LDS ops issued after the producer-word read
             a(f"s_waitcnt lgkmcnt({after})")
             a("v_readfirstlane_b32 s43, v93")
             a("s_cmp_lt_i32 s43, s40")
@@ -132,13 +145,14 @@ def gen_role(IN, OUT_, spec=0, halfpub=True):
             a("v_mov_b32 v64, v92")
             a("ds_write_b32 %[qme], v98")
         else:
-            a(f"s_waitcnt lgkmcnt({nw + 2})")
+            a(f"s_waitcnt lgkmcnt({nw + ncr})")
             a("v_mov_b32 v64, %[ng]")
-        # ---- 32 steps, 8 groups of 4 rows (one v_perm_b32 per column per group)
-        spec_at = 8 - spec // 4 if spec else None
-        for u in range(8):
+        # ---- C steps, C/4 groups of 4 rows (one v_perm_b32 per column per group)
+        ng = C // 4
+        spec_at = ng - spec // 4 if spec else None
+        for u in range(ng):
             if spec and u == spec_at:
-                book(a, p, lds_in, lds_out)
+                book(a, p, lds_in, lds_out, C)
                 a("ds_read_b32 v93, %[pin]")
                 a("ds_read_b32 v92, v95")
             a(f"v_perm_b32 v72, %[pA], %[k80], v{cur + u}")
@@ -146,10 +160,10 @@ def gen_role(IN, OUT_, spec=0, halfpub=True):
             for b in range(4):
                 io, l0 = ("v64", "v65") if b % 2 == 0 else ("v65", "v64")
                 step(a, io, l0, b)
-            if gran and halfpub and u == 3:
-                granule(a)
+            if gran and halfpub and u == ng // 2 - 1:
+                granule(a, grows)
         if not spec:
-            book(a, p, lds_in, lds_out)
+            book(a, p, lds_in, lds_out, C)
     a("s_cmp_lt_i32 s40, %[end]")
     a("s_cbranch_scc1 L_loop_%=")
     # ---- exit: the last chunk's outflow, then every row is out
@@ -162,7 +176,7 @@ def gen_role(IN, OUT_, spec=0, halfpub=True):
         a(f"v_mov_b32 v97, {BIG:#x}")
         a("ds_write_b32 %[pout], v97")
     if gran:
-        granule(a)
+        granule(a, grows)
     a("s_waitcnt vmcnt(0) lgkmcnt(0)")
     a("v_mov_b32 %[M], v74")
     a("s_mov_b32 %[fail], s45")
@@ -179,19 +193,19 @@ def gen_role(IN, OUT_, spec=0, halfpub=True):
     return L
 
 
-def book(a, p, lds_in, lds_out):
+def book(a, p, lds_in, lds_out, C=32):
     """Advance k0, the ring offset and the words to the next chunk."""
-    a("s_add_i32 s40, s40, 32")
-    a("s_add_u32 s41, s41, 0x80")
+    a(f"s_add_i32 s40, s40, {C}")
+    a(f"s_add_u32 s41, s41, {4 * C:#x}")
     a(f"s_and_b32 s41, s41, {(R - 1) * 4:#x}")
     if lds_out:
         a("v_add_u32 v96, s41, %[lout]")
-        a("v_add_u32 v97, 32, v97")
+        a(f"v_add_u32 v97, {C}, v97")
     if lds_in:
         a("v_add_u32 v95, s41, %[lin]")
-        a("v_add_u32 v98, 32, v98")
+        a(f"v_add_u32 v98, {C}, v98")
     if p == 1:
-        a("v_add_u32 v94, 64, v94")
+        a(f"v_add_u32 v94, {2 * C}, v94")
 
 
 def slow_wait(a, label, resume, vreg, addr, sreg, reread=None):
@@ -227,13 +241,339 @@ CLOBBERS = ['"v%d"' % r for r in range(64, 107) if r not in (75, 102, 103, 104)]
 
 def emit(spec=0, halfpub=True):
     out = ["// GENERATED by tools/gen_flow3.py -- do not edit.  The flow3 chunk loops (sw_flow3.hip):",
-           "// one inline-asm block per strip role, R = %d ring rows, SPEC = %d, HALFPUB = %d." % (R, spec, halfpub),
+           "// one inline-asm block per (chunk rows C, strip role), R = %d ring rows, SPEC = %d, HALFPUB = %d."
+           % (R, spec, halfpub),
            "// Operands: see F3Loop in sw_flow3.hip; fixed registers: tools/gen_flow3.py.",
            "#pragma once", ""]
-    for IN in ROLES_IN:
+    for C in (32, 16):
+        for IN in ROLES_IN:
+            for OUT_ in ROLES_OUT:
+                body = gen_role(IN, OUT_, spec, halfpub, C)
+                out.append("template <> __device__ __forceinline__ F3Res f3_loop<%d, F3_%s, F3_%s>(const F3Loop& x) {"
+                           % (C, IN.upper(), OUT_.upper()))
+                out.append("    F3Res r;")
+                out.append("    asm volatile(")
+                for line in body:
+                    out.append('        "%s\\n\\t"' % line)
+                out.append('        : [M] "=v"(r.M), [fail] "=s"(r.fail), [slow] "=s"(r.slow)')
+                out.append('        : [pA] "v"(x.pA), [pB] "v"(x.pB), [ng] "v"(x.ng), [G] "s"(x.G), [k80] "s"(x.k80),')
+                out.append('          [code] "v"(x.code), [lin] "v"(x.lin), [lout] "v"(x.lout), [pin] "v"(x.pin),')
+                out.append('          [pout] "v"(x.pout), [qme] "v"(x.qme), [qnx] "v"(x.qnx), [end] "s"(x.end),')
+                out.append('          [dlo] "s"(x.dlo), [dhi] "s"(x.dhi), [rsrc] "s"(x.rsrc), [ek] "s"(x.ek),')
+                out.append('          [lrow] "v"(x.lrow), [m48] "s"(x.m48)')
+                out.append("        : " + ", ".join(CLOBBERS) + ");")
+                out.append("    return r;")
+                out.append("}")
+                out.append("")
+    return "\n".join(out)
+
+# ============================================================================================
+# Ring mode (C5: one pair N = 2^20, rows streamed, group edges through per-block rings):
+# sw_flow3.hip sw_flow3r_kernel, sw_flow3r_loops.inc.  C = 64, no loader wave, up to 4
+# workgroups per CU (the block's fixed registers stay below v108 so that 128 VGPRs suffice).
+#   v40/v41 IO / L0, v42..v50 step (RING below), v[52:67] / v[68:83] row codes of the even /
+#   odd chunk, v[84:85] granule inflow {H-G, key} (IN=GRAN) or LDS inflow row (v84), v86
+#   producer word read, v87 code read address, v88 / v89 LDS inflow / outflow address,
+#   v90 / v91 producer / consumer word values, v92 back-pressure read, v93 raw row byte,
+#   v94 row code, v95 code write address, v[96:97] granule outflow, v98 its slot offset,
+#   v99 its masked offset, v100 its position << 5, v101 granule inflow offset, v102 its
+#   position << 5, v103 scratch, v104 consumer report, v105 code read offset, v106 raw row,
+#   v107 granule outflow row;  s40 k0, s41 / s42 LDS out / in ring offset, s43 producer word,
+#   s44 LDS consumer word, s45 failed, s46 slow-path count, s[48:49] clock, s[50:51] /
+#   s[56:57] masks, s52 HBM consumer word, s53 code slot base, s54 / s55 scratch, s[58:59]
+#   live lanes.
+# Granules (ring edges): 8 B {H-G, (H-G) ^ epoch ^ 0x5BD1E995 ^ (position << 5)} at slot * 8;
+# the position term rejects a slot still holding an earlier round's row (same epoch).
+# ============================================================================================
+RR = 512                 # LDS ring rows per in-workgroup link (sw_flow3.hip F3R_R)
+RING = dict(H="v42", HGO="v43", HB="v44", HGOB="v45", TA="v46", TB="v47", PA="v48", PB="v49", M="v50")
+
+
+def ring_granule(a):
+    """Publish lanes 32..63 of IO (the 32 newest outflow rows, row v107) as 8-B granules
+    at their ring slots, rows outside [0, m) dropped."""
+    a("v_mov_b32 v96, v40")
+    a("v_xor_b32 v97, %[ek], v40")
+    a("v_xor_b32 v97, v97, v100")
+    a("v_cmp_gt_u32_e64 s[50:51], %[m], v107")          # 0 <= row < m (unsigned)
+    a("s_and_b64 s[50:51], s[50:51], %[lhi]")
+    a("v_cndmask_b32_e64 v99, -16, v98, s[50:51]")
+    a("v_add_u32 v98, 0x100, v98")                      # 32 rows on
+    a("v_and_b32 v98, %[gomask8], v98")
+    a("v_add_u32 v100, 0x400, v100")
+    a("v_add_u32 v107, 32, v107")
+    a("buffer_store_dwordx2 v[96:97], v99, %[gors], 0 offen sc1")
+
+
+def ring_gin_check(a):
+    """s[58:59] = live lanes (row k0 + lane < m); s[50:51] = live lanes whose granule fails."""
+    a("s_sub_i32 s54, %[m], s40")
+    a("v_cmp_gt_i32_e64 s[58:59], s54, %[lane]")
+    a("v_xor_b32 v103, v84, v85")
+    a("v_xor_b32 v103, v103, v102")
+    a("v_cmp_ne_u32_e64 s[56:57], %[ek], v103")
+    a("s_and_b64 s[50:51], s[58:59], s[56:57]")
+    a("s_cmp_lg_u64 s[50:51], 0")
+
+
+def gen_role_ring(IN, OUT_):
+    L = []
+    a = L.append
+    lds_in, lds_out = IN == "lds", OUT_ == "lds"
+    gin, gout = IN == "gran", OUT_ == "gran"
+    # ---- entry (s_nop 4: descriptor operands may be fresh from v_readfirstlane)
+    a("s_nop 4")
+    a("s_waitcnt vmcnt(0) lgkmcnt(0)")
+    for r in ("v42", "v43", "v44", "v45", "v50"):
+        a(f"v_mov_b32 {r}, 0")
+    a("v_mov_b32 v40, %[ng]")
+    a("v_mov_b32 v41, %[ng]")
+    a("v_mov_b32 v93, %[raw2]")                      # raw bytes of chunk 2 (loaded by the caller)
+    a("v_mov_b32 v105, %[cro]")
+    a("v_mov_b32 v106, %[rrow]")
+    a("s_mov_b32 s40, 0")
+    a("s_mov_b32 s41, 0")
+    a("s_movk_i32 s42, 0x200")                       # ((0 + 128) mod R) * 4
+    a("s_movk_i32 s53, 0xc0")                        # slot base of chunk 2's codes: ((0 + 3) & 3) * 64
+    a("s_mov_b32 s45, 0")
+    a("s_mov_b32 s46, 0")
+    a(f"s_movk_i32 s44, {RR}")
+    a("s_mov_b32 s52, 0")
+    if lds_out:
+        a("v_mov_b32 v90, 0xffffff80")              # producer word at chunk 0: k0 - 128
+        a("v_add_u32 v89, s41, %[lout]")
+    if lds_in:
+        a(f"v_mov_b32 v91, {RR + 64}")              # consumer word after chunk 0: 64 consumed (+ R)
+        a("v_add_u32 v88, s42, %[lin]")
+    if gout:
+        a("v_mov_b32 v98, %[gooff]")
+        a("v_mov_b32 v100, %[gopos]")
+        a("v_mov_b32 v107, %[gorow]")
+    if gin:
+        a("v_mov_b32 v101, %[gioff]")
+        a("v_mov_b32 v102, %[gipos]")
+        a("buffer_load_dwordx2 v[84:85], v101, %[girs], 0 offen sc1")
+    a("ds_read_b128 v[52:55], %[c0]")
+    a("ds_read_b128 v[56:59], %[c0] offset:16")
+    a("ds_read_b128 v[60:63], %[c0] offset:32")
+    a("ds_read_b128 v[64:67], %[c0] offset:48")
+    a("s_waitcnt vmcnt(0) lgkmcnt(0)")
+    a("L_loop_%=:")
+    for p in (0, 1):
+        cur = 52 if p == 0 else 68
+        nxt = 68 if p == 0 else 52
+        lds = []                                      # LDS ops of this chunk top, in issue order
+        # 1. publish the last chunk's outflow
+        if lds_out:
+            if p == 0:
+                a("s_cmp_lt_i32 s44, s40")
+                a(f"s_cbranch_scc1 L_bp{p}_%=")
+                a(f"L_bpr{p}_%=:")
+            a("ds_write_b32 v89, v40")
+            a("ds_write_b32 %[pout], v90")
+            lds += ["W1", "W2"]
+        if gout:
+            a("s_add_u32 s55, s40, %[bpbase]")
+            a("s_sub_u32 s54, s52, s55")
+            a("s_cmp_lt_i32 s54, 0")
+            a(f"s_cbranch_scc1 L_bpg{p}_%=")
+            a(f"L_bpgr{p}_%=:")
+            ring_granule(a)
+        # 2. this chunk's inflow words / rows (LDS)
+        if lds_in:
+            a("ds_read_b32 v86, %[pin]")
+            a("ds_read_b32 v84, v88")
+            lds += ["A", "B"]
+        # 3. the raw bytes of chunk c+2 and the granules of chunk c (loaded one chunk ago)
+        stores_after = (2 if gout else 0) + (1 if gin and p == 0 else 0)   # stores issued after those loads
+        a(f"s_waitcnt vmcnt({stores_after})")
+        if gin:
+            ring_gin_check(a)
+            a(f"s_cbranch_scc1 L_gin{p}_%=")
+            a(f"L_ginr{p}_%=:")
+            a("v_cndmask_b32_e64 v40, %[ng], v84, s[58:59]")
+        elif not lds_in:
+            a("v_mov_b32 v40, %[ng]")
+        # 4. codes of chunk c+2 into the wave's code ring (slot base s53, mirror of slots [0, 64))
+        a("v_lshrrev_b32 v94, 1, v93")
+        a("v_lshrrev_b32 v103, 2, v93")
+        a("v_xor_b32 v94, v94, v103")
+        a("v_and_or_b32 v94, v94, 3, 4")
+        a("v_cmp_ne_u32_e64 s[56:57], 0, v93")
+        a("v_cndmask_b32_e64 v94, 0, v94, s[56:57]")
+        a("v_add_u32 v95, s53, %[cwr]")
+        a("ds_write_b8 v95, v94")
+        a("s_cmp_eq_u32 s53, 0")
+        a("s_cselect_b32 s54, 0, 64")                # the mirror (slots 256..319) or the sink (320..383)
+        a("v_add_u32 v95, s54, %[cwm]")
+        a("ds_write_b8 v95, v94")
+        a("s_add_u32 s53, s53, 64")
+        a("s_and_b32 s53, s53, 0xff")
+        lds += ["C1", "C2"]
+        # 5. raw bytes of chunk c+3, granules of chunk c+1
+        a("v_add_u32 v106, 64, v106")
+        a("buffer_load_ubyte v93, v106, %[rrs], 0 offen")
+        if gin:
+            a("v_add_u32 v101, 0x200, v101")
+            a("v_and_b32 v101, %[gimask8], v101")
+            a("v_add_u32 v102, 0x800, v102")
+            a("buffer_load_dwordx2 v[84:85], v101, %[girs], 0 offen sc1")
+            if p == 1:   # every other chunk: rows consumed (for the producer's back-pressure)
+                a("s_add_u32 s54, s40, 64")
+                a("s_min_i32 s54, s54, %[m]")
+                a("s_add_u32 s54, s54, %[crv0]")
+                a("v_mov_b32 v104, s54")
+                a("buffer_store_dword v104, %[croff], %[cross], 0 offen sc1")
+        # 6. row codes of chunk c+1
+        a("v_add_u32 v87, %[cbase], v105")
+        for q in range(4):
+            a(f"ds_read_b128 v[{nxt + 4 * q}:{nxt + 4 * q + 3}], v87 offset:{16 * q}" if q else
+              f"ds_read_b128 v[{nxt}:{nxt + 3}], v87")
+        a("v_add_u32 v105, 64, v105")
+        a("v_and_b32 v105, 0xff, v105")
+        lds += ["N1", "N2", "N3", "N4"]
+        # 7. LDS inflow: word check, rows into IO, consumed word
+        if lds_in:
+            after_a = len(lds) - 1 - lds.index("A")
+            a(f"s_waitcnt lgkmcnt({after_a})")
+            a("v_readfirstlane_b32 s43, v86")
+            a("s_cmp_lt_i32 s43, s40")
+            a(f"s_cbranch_scc1 L_in{p}_%=")
+            a(f"L_inr{p}_%=:")
+            a(f"s_waitcnt lgkmcnt({after_a - 1})")
+            a("v_mov_b32 v40, v84")
+            a("ds_write_b32 %[qme], v91")
+        else:
+            # this chunk's codes (read one chunk ago) must be in: every LDS op since is younger
+            a(f"s_waitcnt lgkmcnt({len(lds)})")
+        # 8. 64 steps, 16 groups of 4 rows
+        for u in range(16):
+            a(f"v_perm_b32 v48, %[pA], %[k80], v{cur + u}")
+            a(f"v_perm_b32 v49, %[pB], %[k80], v{cur + u}")
+            for b in range(4):
+                io, l0 = ("v40", "v41") if b % 2 == 0 else ("v41", "v40")
+                step(a, io, l0, b, RING)
+            if gout and u == 7:
+                ring_granule(a)
+        # 9. on to the next chunk
+        a("s_add_i32 s40, s40, 64")
+        if lds_out:
+            a("s_add_u32 s41, s41, 0x100")
+            a(f"s_and_b32 s41, s41, {(RR - 1) * 4:#x}")
+            a("v_add_u32 v89, s41, %[lout]")
+            a("v_add_u32 v90, 64, v90")
+        if lds_in:
+            a("s_add_u32 s42, s42, 0x100")
+            a(f"s_and_b32 s42, s42, {(RR - 1) * 4:#x}")
+            a("v_add_u32 v88, s42, %[lin]")
+            a("v_add_u32 v91, 64, v91")
+    a("s_cmp_lt_i32 s40, %[end]")
+    a("s_cbranch_scc1 L_loop_%=")
+    # ---- exit
+    if lds_out:
+        a("s_cmp_lt_i32 s44, s40")
+        a("s_cbranch_scc1 L_bpx_%=")
+        a("L_bpxr_%=:")
+        a("ds_write_b32 v89, v40")
+        a(f"v_mov_b32 v90, {BIG:#x}")
+        a("ds_write_b32 %[pout], v90")
+    if gout:
+        a("s_add_u32 s55, s40, %[bpbase]")
+        a("s_sub_u32 s54, s52, s55")
+        a("s_cmp_lt_i32 s54, 0")
+        a("s_cbranch_scc1 L_bpgx_%=")
+        a("L_bpgxr_%=:")
+        ring_granule(a)
+    if gin:   # every row consumed
+        a("s_add_u32 s54, %[m], %[crv0]")
+        a("v_mov_b32 v104, s54")
+        a("buffer_store_dword v104, %[croff], %[cross], 0 offen sc1")
+    a("s_waitcnt vmcnt(0) lgkmcnt(0)")
+    a("v_mov_b32 %[M], v50")
+    a("s_mov_b32 %[fail], s45")
+    a("s_mov_b32 %[slow], s46")
+    a("s_branch L_done_%=")
+    # ---- slow paths
+    if lds_in:
+        for p in (0, 1):
+            slow_wait(a, f"L_in{p}_%=", f"L_inr{p}_%=", "v86", "%[pin]", "s43", reread="ds_read_b32 v84, v88")
+    if lds_out:
+        slow_wait(a, "L_bp0_%=", "L_bpr0_%=", "v92", "%[qnx]", "s44")
+        slow_wait(a, "L_bpx_%=", "L_bpxr_%=", "v92", "%[qnx]", "s44")
+    if gout:
+        for lab, res in (("L_bpg0_%=", "L_bpgr0_%="), ("L_bpg1_%=", "L_bpgr1_%="), ("L_bpgx_%=", "L_bpgxr_%=")):
+            slow_bp_hbm(a, lab, res)
+    if gin:
+        for p in (0, 1):
+            slow_gin(a, f"L_gin{p}_%=", f"L_ginr{p}_%=")
+    a("L_done_%=:")
+    return L
+
+
+def slow_timeout(a, label):
+    """s[48:49] = s_memrealtime (waited): on to {label}_w unless past the deadline, then fail."""
+    a("s_sub_u32 s48, s48, %[dlo]")
+    a("s_subb_u32 s49, s49, %[dhi]")
+    a("s_cmp_lt_i32 s49, 0")
+    a("s_cbranch_scc0 %s_x" % label)
+    a("s_sleep 1")
+    a(f"s_branch {label}_w")
+
+
+def slow_bp_hbm(a, label, resume):
+    """The consumer of a ring edge has not yet reported the rows this publish overwrites:
+    re-read its word (HBM, sc1) until it covers them (serial-number compare)."""
+    a(f"{label}:")
+    a("s_add_u32 s46, s46, 1")
+    a("s_cmp_lg_u32 s45, 0")
+    a(f"s_cbranch_scc1 {resume}")
+    a(f"{label}_w:")
+    a("buffer_load_dword v92, off, %[bpr], 0 sc1")
+    a("s_memrealtime s[48:49]")
+    a("s_waitcnt vmcnt(0) lgkmcnt(0)")
+    a("v_readfirstlane_b32 s52, v92")
+    a("s_add_u32 s55, s40, %[bpbase]")
+    a("s_sub_u32 s54, s52, s55")
+    a("s_cmp_ge_i32 s54, 0")
+    a(f"s_cbranch_scc1 {resume}")
+    slow_timeout(a, label)
+    a(f"{label}_x:")
+    a("s_mov_b32 s45, 1")
+    a(f"s_branch {resume}")
+
+
+def slow_gin(a, label, resume):
+    """The chunk's inflow granules are not all published yet: re-load and re-check."""
+    a(f"{label}:")
+    a("s_add_u32 s46, s46, 1")
+    a("s_cmp_lg_u32 s45, 0")
+    a(f"s_cbranch_scc1 {resume}")
+    a(f"{label}_w:")
+    a("buffer_load_dwordx2 v[84:85], v101, %[girs], 0 offen sc1")
+    a("s_memrealtime s[48:49]")
+    a("s_waitcnt vmcnt(0) lgkmcnt(0)")
+    ring_gin_check(a)
+    a(f"s_cbranch_scc0 {resume}")
+    slow_timeout(a, label)
+    a(f"{label}_x:")
+    a("s_mov_b32 s45, 1")
+    a(f"s_branch {resume}")
+
+
+ROLES_IN_RING = ("none", "lds", "gran")
+CLOBBERS_RING = ['"v%d"' % r for r in range(40, 108) if r != 51] + \
+    ['"s%d"' % r for r in range(40, 60) if r not in (47,)] + ['"scc"', '"vcc"', '"memory"']
+
+
+def emit_ring():
+    out = ["// GENERATED by tools/gen_flow3.py -- do not edit.  The flow3 ring-mode chunk loops",
+           "// (sw_flow3.hip sw_flow3r_kernel): one inline-asm block per strip role, C = 64, R = %d." % RR,
+           "// Operands: see F3RLoop in sw_flow3.hip; fixed registers: tools/gen_flow3.py.",
+           "#pragma once", ""]
+    for IN in ROLES_IN_RING:
         for OUT_ in ROLES_OUT:
-            body = gen_role(IN, OUT_, spec, halfpub)
-            out.append("template <> __device__ __forceinline__ F3Res f3_loop<F3_%s, F3_%s>(const F3Loop& x) {"
+            body = gen_role_ring(IN, OUT_)
+            out.append("template <> __device__ __forceinline__ F3Res f3r_loop<F3_%s, F3_%s>(const F3RLoop& x) {"
                        % (IN.upper(), OUT_.upper()))
             out.append("    F3Res r;")
             out.append("    asm volatile(")
@@ -241,30 +581,42 @@ def emit(spec=0, halfpub=True):
                 out.append('        "%s\\n\\t"' % line)
             out.append('        : [M] "=v"(r.M), [fail] "=s"(r.fail), [slow] "=s"(r.slow)')
             out.append('        : [pA] "v"(x.pA), [pB] "v"(x.pB), [ng] "v"(x.ng), [G] "s"(x.G), [k80] "s"(x.k80),')
-            out.append('          [code] "v"(x.code), [lin] "v"(x.lin), [lout] "v"(x.lout), [pin] "v"(x.pin),')
-            out.append('          [pout] "v"(x.pout), [qme] "v"(x.qme), [qnx] "v"(x.qnx), [end] "s"(x.end),')
-            out.append('          [dlo] "s"(x.dlo), [dhi] "s"(x.dhi), [rsrc] "s"(x.rsrc), [ek] "s"(x.ek),')
-            out.append('          [lrow] "v"(x.lrow), [m48] "s"(x.m48)')
-            out.append("        : " + ", ".join(CLOBBERS) + ");")
+            out.append('          [m] "s"(x.m), [end] "s"(x.end), [dlo] "s"(x.dlo), [dhi] "s"(x.dhi), [lane] "v"(x.lane),')
+            out.append('          [raw2] "v"(x.raw2), [cro] "v"(x.cro), [c0] "v"(x.c0), [cbase] "v"(x.cbase),')
+            out.append('          [cwr] "v"(x.cwr), [cwm] "v"(x.cwm), [rrs] "s"(x.rrs), [rrow] "v"(x.rrow),')
+            out.append('          [lin] "v"(x.lin), [lout] "v"(x.lout), [pin] "v"(x.pin), [pout] "v"(x.pout),')
+            out.append('          [qme] "v"(x.qme), [qnx] "v"(x.qnx),')
+            out.append('          [girs] "s"(x.girs), [gioff] "v"(x.gioff), [gipos] "v"(x.gipos), [gimask8] "s"(x.gimask8),')
+            out.append('          [ek] "s"(x.ek), [cross] "s"(x.cross), [crv0] "s"(x.crv0), [croff] "v"(x.croff),')
+            out.append('          [gors] "s"(x.gors), [gooff] "v"(x.gooff), [gopos] "v"(x.gopos), [gomask8] "s"(x.gomask8),')
+            out.append('          [gorow] "v"(x.gorow), [lhi] "s"(x.lhi), [bpr] "s"(x.bpr), [bpbase] "s"(x.bpbase)')
+            out.append("        : " + ", ".join(CLOBBERS_RING) + ");")
             out.append("    return r;")
             out.append("}")
             out.append("")
     return "\n".join(out)
 
 
+OUT_RING = os.path.join(ROOT, "concurrentproject_amd", "csrc", "sw_flow3r_loops.inc")
+
+
 def main():
     spec = int(os.environ.get("F3_SPEC", "4"))
     halfpub = os.environ.get("F3_HALFPUB", "1") != "0"
     text = emit(spec, halfpub)
+    text_ring = emit_ring()
     if "--check" in sys.argv:
         cur = open(OUT).read() if os.path.exists(OUT) else ""
-        sys.exit(0 if cur == text else 1)
+        cur_r = open(OUT_RING).read() if os.path.exists(OUT_RING) else ""
+        sys.exit(0 if cur == text and cur_r == text_ring else 1)
     path = OUT
     for i, arg in enumerate(sys.argv):
         if arg == "-o":
             path = sys.argv[i + 1]
     with open(path, "w") as f:
         f.write(text)
+    with open(OUT_RING, "w") as f:
+        f.write(text_ring)
 
 
 if __name__ == "__main__":
