@@ -189,8 +189,9 @@ void sw_db_close(sw_db* db);
  *   "f2pwg"    DNA batches whose scores need int32 (no 16-bit duos): -1 = (default) the
  *              flow2 step with a pair per workgroup when its constants fit, 0 = never
  *              (the pair-per-workgroup strip kernel), 1 = also for a forced mode 5 batch
- *   "f3"       1 = (default) a staged two-column linear-gap flow2 launch (C = 32: C2) runs the
- *              flow3 kernel (hand-scheduled chunk loops), 0 = the compiled flow2 kernel
+ *   "f3"       1 = (default) a two-column linear-gap flow2 launch runs the flow3 kernel
+ *              (hand-scheduled chunk loops): staged codes at C = 32 / 16 (C2), ring edges at
+ *              C = 64 (C5); 0 = the compiled flow2 kernel
  *   "slab_plain" 1 = an exported slab buffer may fall back to plain device memory (one-GPU
  *              tests only; cross-GPU edges need fine-grained memory), 0 = (default) refuse
  *   "trace"    device address of a 16 x u64 per-strip trace buffer, 0 = off (tools)
