@@ -64,7 +64,7 @@ Params g_params;
 
 std::atomic<long long> g_opt_W{0}, g_opt_C{0}, g_opt_bytes{0}, g_opt_timeout{30}, g_opt_blocks{0}, g_opt_orient{0},
     g_opt_mode{-1}, g_opt_trace{0}, g_opt_duo_f16{1}, g_opt_f2stream{0}, g_opt_ring{-1}, g_opt_ring_rows{4096}, g_opt_f2_wgs{0}, g_opt_f2w{0}, g_opt_f2pwg{-1},
-    g_opt_linear{-1}, g_opt_f3{1}, g_opt_slab_plain{0};
+    g_opt_linear{-1}, g_opt_f3{1}, g_opt_slab_plain{0}, g_opt_duo_lds{1}, g_opt_duo_rev{0};
 
 // Longest sequence the engine takes: granule buffers of m rows keep m * 16 in the
 // 32-bit record count of a buffer resource (sw_device.h linear_edge).
@@ -566,7 +566,11 @@ void profile_words(const Params& p, unsigned out[4]) {
 }
 
 int waves_per_cu(Ctx* c, const LaunchCfg& cfg) {
-    const int key = cfg.mode * 100000 + cfg.W * 1000 + cfg.C * 2 + (cfg.dna ? 1 : 0);
+    int lw = 0;   // the duo LDS kernel: its dynamic LDS (wrap slots, slot size) bounds the residency
+    while (cfg.duo_wrap > (1 << lw)) ++lw;
+    const int key = (cfg.duo_wrap > 0 ? (lw * 4 + (cfg.f2_lin ? 1 : 0) + (cfg.duo_f16 ? 2 : 0) + 1) * 1000000 : 0) +
+                    cfg.mode * 100000 +
+                    cfg.W * 1000 + cfg.C * 2 + (cfg.dna ? 1 : 0);
     auto it = c->waves_cache.find(key);
     if (it != c->waves_cache.end()) return it->second;
     int w = cfg.mode == MODE_FLOW2 ? flow2_waves_per_cu(cfg.C) : kernel_waves_per_cu(cfg);
@@ -651,6 +655,18 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
     const bool f3_base = g_opt_f3.load() != 0 && job.mode == MODE_FLOW2 && job.f2w2 && f2_lin && !job.pwg;
     const bool use_f3 = f3_base && ((!f2s && !job.ring && flow3_fits(max_m_f3, job.C)) ||
                                     (job.ring && edge == nullptr && job.C == 64));
+    // duo batches at C = 64: strip hand-offs in LDS when the wrap buffer (a round's rows of
+    // both pairs) fits the default dynamic-LDS limit; no boundary buffers in HBM then
+    int duo_wrap = 0;
+    if (duo && job.C == 64 && g_opt_duo_lds.load() != 0) {
+        int max_mp = 0;
+        for (const DuoDesc& d : job.duos) max_mp = std::max(max_mp, d.m_pad);
+        const int slots = duo_wrap_slots(max_mp);
+        if ((long long)slots * (f2_lin ? 4 : 8) <= DUO_LDS_DYN_MAX) {
+            duo_wrap = slots;
+            job.bnd_granules = 0;
+        }
+    }
     // read once: it sizes the ring arena here and addresses it in the kernel (kp.ring_rows)
     const long long ring_rows = g_opt_ring_rows.load();
     int ring_blocks = 0, wrap_rows = 0;
@@ -728,6 +744,7 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
     // the staged two-column linear-gap kernel with hand-scheduled chunk loops (sw_flow3.hip), unless
     // option f3 = 0: C2
     cfg.f3 = use_f3;
+    cfg.duo_wrap = duo_wrap;
     if (cfg.f2_w2 && job.C == 16 && !use_f3) {
         set_err("flow2: two columns per lane at C = 16 runs on flow3 only (rows staged in LDS, one GPU)");
         return -1;
@@ -788,6 +805,10 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
         for (int r = 0; r < 4; ++r) w |= (unsigned)(r == q ? 0 : prm.match - prm.mismatch) << (8 * r);
         kp.pen[q] = w;
     }
+    if (duo_wrap > 0) {
+        kp.wrap_rows = duo_wrap;
+        kp.duo_rev = g_opt_duo_rev.load() != 0 ? 1 : 0;
+    }
     kp.timeout_ticks = g_opt_timeout.load() * 100000000LL;   // s_memrealtime: 100 MHz
     kp.trace = reinterpret_cast<unsigned long long*>(g_opt_trace.load());
     if (job.ring) {
@@ -816,7 +837,7 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
     t_stats.items = items;
     t_stats.mode = job.mode;
     t_stats.variant = (cfg.duo_f16 ? 1 : 0) | (cfg.f2_stream ? 2 : 0) | (job.ring ? 4 : 0) | (cfg.f2_lin ? 8 : 0) |
-                      (cfg.f2_w2 ? 16 : 0) | (cfg.f2_pwg ? 32 : 0) | (cfg.f3 ? 64 : 0);
+                      (cfg.f2_w2 ? 16 : 0) | (cfg.f2_pwg ? 32 : 0) | (cfg.f3 ? 64 : 0) | (cfg.duo_wrap > 0 ? 128 : 0);
     t_stats.boundary_bytes = (long long)(job.bnd_granules * sizeof(Granule));
     c->last = s;
     return 0;
@@ -1586,6 +1607,12 @@ int sw_set_option(const char* key, long long v) {
     } else if (k == "f3") {   // 1 (default): staged W2 linear-gap launches on flow3 (sw_flow3.hip), 0: flow2
         if (v < 0 || v > 1) return -1;
         g_opt_f3 = v;
+    } else if (k == "duo_lds") {   // 1 (default): duo strip hand-offs in LDS when the wrap buffer fits, 0: HBM granules
+        if (v < 0 || v > 1) return -1;
+        g_opt_duo_lds = v;
+    } else if (k == "duo_rev") {   // 1: the duo LDS kernel's odd workgroups run the strip roles in reverse wave order
+        if (v < 0 || v > 1) return -1;
+        g_opt_duo_rev = v;
     } else if (k == "slab_plain") {   // 1: exported slab buffers may fall back to plain device memory
         if (v < 0 || v > 1) return -1;
         g_opt_slab_plain = v;
@@ -1623,6 +1650,8 @@ long long sw_get_option(const char* key) {
     if (k == "f2pwg") return g_opt_f2pwg;
     if (k == "f3") return g_opt_f3;
     if (k == "slab_plain") return g_opt_slab_plain;
+    if (k == "duo_lds") return g_opt_duo_lds;
+    if (k == "duo_rev") return g_opt_duo_rev;
     return -1;
 }
 

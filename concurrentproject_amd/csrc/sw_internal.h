@@ -96,6 +96,8 @@ struct KParams {
     int ring_rows;
     int wrap_rows;
     unsigned* ring_cons;          // ring j's consumer progress (positions consumed), RING_CONS_STRIDE apart
+    // (the duo kernel with LDS hand-offs takes its wrap-buffer slots from wrap_rows)
+    int duo_rev;                  // duo LDS kernel: odd workgroups map strip roles to waves in reverse
 };
 
 constexpr int RING_CONS_STRIDE = 32;   // dwords between consumer progress words (one 128-B line each)
@@ -132,7 +134,16 @@ struct LaunchCfg {
     bool f2_w2 = false;     // MODE_FLOW2 with f2_lin: two columns per lane (126 new columns per strip)
     bool f2_pwg = false;    // MODE_FLOW2 batch: a pair per workgroup, all hand-offs in LDS (C = 64, streamed)
     bool f3 = false;        // MODE_FLOW2 staged two-column linear-gap launch on the flow3 kernel (sw_flow3.hip)
+    int duo_wrap = 0;       // MODE_DUO at C = 64: > 0 = strip hand-offs in LDS (sw_duo_lds_kernel), this many
+                            // wrap-buffer slots (a power of two >= every m_pad); 0 = HBM granules
 };
+// the duo LDS kernel's wrap buffer: slots for rows of m_pad up to m, and its dynamic LDS
+inline int duo_wrap_slots(int m) {
+    int w = 64;
+    while (w < m) w *= 2;
+    return w;
+}
+constexpr int DUO_LDS_DYN_MAX = 64 * 1024;   // within the default dynamic-LDS limit, two workgroups per CU
 constexpr int F2_WGS_MAX = 4;   // flow2 streamed kernel: most workgroups per CU (launch_c sizes the LDS pad)
 
 // MODE_FLOW stages a pair's row codes in LDS: one byte per row plus the

@@ -938,10 +938,178 @@ __global__ void __launch_bounds__(64 * DUO_WAVES) sw_duo_kernel(KParams kp) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// The duo kernel with every strip hand-off in LDS (LaunchCfg::duo_wrap > 0, C = 64):
+// as sw_duo_kernel, wave w runs strips w, w + 4, ... of each duo, one per round, but
+// strip s hands its right edge to strip s + 1 through the workgroup's LDS instead of
+// HBM granules:
+//   * wave w -> w + 1 (same round): a DUO_R-row ring, row r at slot (pos0 + r) mod R,
+//     with back-pressure on the consumer's progress word;
+//   * wave 3 -> wave 0 (next round): the wrap buffer, kp.wrap_rows >= m slots (dynamic
+//     LDS), without back-pressure: wave 3 writes row r of round k + 1 only after waves
+//     2, 1, 0 of round k + 1 have computed row r, so wave 0 has read row r of round k
+//     by then (a back-pressure wait there would close the cycle 0 -> 1 -> 2 -> 3 -> 0).
+// Positions: round k of the workgroup's duo sequence starts at the sum of the spans of
+// the rounds before it (every wave walks the same rounds), so progress words grow
+// monotonically across rounds and duos and the waves need no barrier between duos.
+// A slot holds the edge's A (= H + MATCH) of both pairs, and with the affine step E too.
+// ---------------------------------------------------------------------------
+constexpr int DUO_R = 256;   // rows per in-round ring (a link's lag is ~C rows)
+template <bool LIN> struct DuoSlotT { using T = uint2; };
+template <> struct DuoSlotT<true> { using T = unsigned; };
+template <bool LIN> using DuoSlot = typename DuoSlotT<LIN>::T;
+
+template <bool LIN>
+struct DuoLink {
+    DuoSlot<LIN>* buf;   // ring or wrap buffer
+    unsigned mask;       // row r at slot (off + r) & mask
+    int off;
+    int pb;              // position of row 0 in the progress words
+    const int* prod;     // inflow: the producer's word (rows < *prod - pb are written)
+    const int* cons;     // outflow ring: the consumer's word (positions < *cons are read); null: none
+};
+
+template <int W, int C, bool M3, bool LIN>
+__device__ void strip_pass_duo_lds(const KParams& kp, const DuoDesc& d, const int strip, const int lane,
+                                   const bool has_in, const DuoLink<LIN> in, const bool has_out,
+                                   const DuoLink<LIN> out, int* const prod_out, int* const cons_out,
+                                   DuoSlot<LIN>* const sink) {
+    constexpr int SW = 64 * W;
+    static_assert(C == 64, "the LDS links move one row per lane and chunk");
+    const int m = d.m_pad;
+    const u16x2 go2 = splat2(kp.gap_init), ge2 = splat2(kp.gap_ext), ma2 = splat2(kp.match),
+                gom2 = splat2(kp.gap_init + kp.match);
+    StripDuo<W, M3, LIN> S;
+    S.setup(kp, d, strip, lane);
+    const __amdgpu_buffer_rsrc_t r0 =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned char*>(kp.seq + d.row_off[0]), 0, d.m[0], RSRC_FLAGS);
+    const __amdgpu_buffer_rsrc_t r1 =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned char*>(kp.seq + d.row_off[1]), 0, d.m[1], RSRC_FLAGS);
+    const int nchunks = (m + SW - 1 + C - 1) / C;
+    const long long t_start = (long long)__builtin_amdgcn_s_memrealtime();
+    bool failed = false;
+    int cons_seen = 0;
+    unsigned raw0_nxt = fetch_raw(r0, 0, lane, C, d.m[0]), raw1_nxt = fetch_raw(r1, 0, lane, C, d.m[1]);
+    for (int c = 0; c < nchunks; ++c) {
+        const int k0 = c * C;
+        const unsigned raw0 = raw0_nxt, raw1 = raw1_nxt;
+        raw0_nxt = fetch_raw(r0, k0 + C, lane, C, d.m[0]);
+        raw1_nxt = fetch_raw(r1, k0 + C, lane, C, d.m[1]);
+        unsigned va = as32(ma2), ve = 0u;   // no inflow / rows >= m: the border (H = E = 0)
+        if (has_in) {
+            // the progress word and the chunk's rows in one LDS round trip (a wave's DS ops
+            // execute in order: rows read after a word that covers them are complete)
+            const int need = in.pb + min(k0 + C, m);
+            DuoSlot<LIN>* const src = &in.buf[(unsigned)(in.off + k0 + lane) & in.mask];
+            int avail = lds_load(in.prod);
+            compiler_fence();
+            DuoSlot<LIN> v = *src;
+            if (__builtin_amdgcn_readfirstlane(avail) < need && !failed) {
+                do {
+                    __builtin_amdgcn_s_sleep(1);
+                    avail = lds_load(in.prod);
+                    compiler_fence();
+                    v = *src;
+                    if ((long long)__builtin_amdgcn_s_memrealtime() - t_start > kp.timeout_ticks) {
+                        failed = true;
+                        break;
+                    }
+                } while (__builtin_amdgcn_readfirstlane(avail) < need);
+            }
+            const bool real = k0 + lane < m;
+            if constexpr (LIN) {
+                va = real ? v : va;
+            } else {
+                va = real ? v.x : va;
+                ve = real ? v.y : 0u;
+            }
+            compiler_fence();
+            *cons_out = in.pb + k0 + C;   // after the ring read (DS ops execute in order)
+        }
+        S.IOA = va;
+        S.IOE = ve;
+        S.IOR = codes_duo(raw0, raw1, k0, lane, C, d);
+        S.template run<C>(go2, ge2, ma2, gom2);
+        if (has_out) {
+            // lane L holds the outflow of step k0 + L: row k0 + L - (SW - 1)
+            const int row_out = k0 + lane - (SW - 1);
+            if (out.cons != nullptr) {
+                // this chunk's last position reuses the slot of position last - R: read by now?
+                const int floor_pos = out.pb + k0 + C - SW + 1 - DUO_R;
+                if (cons_seen < floor_pos && !failed) {
+                    cons_seen = __builtin_amdgcn_readfirstlane(lds_load(out.cons));
+                    while (cons_seen < floor_pos) {
+                        __builtin_amdgcn_s_sleep(1);
+                        cons_seen = __builtin_amdgcn_readfirstlane(lds_load(out.cons));
+                        if ((long long)__builtin_amdgcn_s_memrealtime() - t_start > kp.timeout_ticks) {
+                            failed = true;
+                            break;
+                        }
+                    }
+                }
+            }
+            const bool st = row_out >= 0 && row_out < m;
+            DuoSlot<LIN>* const dst = st ? &out.buf[(unsigned)(out.off + row_out) & out.mask] : &sink[lane];
+            if constexpr (LIN) *dst = S.IOA;
+            else *dst = make_uint2(S.IOA, S.IOE);
+            compiler_fence();
+            *prod_out = out.pb + min(max(0, k0 + C - SW + 1), m);   // after the slot writes
+        }
+    }
+    if (failed && lane == 0) {
+        atomicOr(&kp.ctrl->error, ERR_TIMEOUT);
+        atomicMax(&kp.ctrl->err_item, (unsigned)strip);
+    }
+    S.commit_max(kp, d, lane);
+}
+
+// kp.wrap_rows: slots of the wrap buffer (a power of two >= every duo's m_pad);
+// kp.duo_rev: odd workgroups run the strip roles in reverse wave order (see LaunchCfg)
+template <int W, int C, bool M3, bool LIN>
+__global__ void __launch_bounds__(64 * DUO_WAVES) sw_duo_lds_kernel(KParams kp) {
+    static_assert(DUO_WAVES == 4, "the LDS links pair waves w -> w + 1 and 3 -> 0");
+    using Slot = DuoSlot<LIN>;
+    extern __shared__ __attribute__((aligned(16))) unsigned char duo_dyn[];
+    Slot* const wrap = reinterpret_cast<Slot*>(duo_dyn);
+    __shared__ Slot ring[3][DUO_R];
+    __shared__ Slot sink[4][64];
+    __shared__ int prod[4], cons[4], psink[4][64];
+    const int lane = threadIdx.x & 63;
+    const int hw = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int wave = kp.duo_rev && (blockIdx.x & 1) ? 3 - hw : hw;
+    if (threadIdx.x < 4) {
+        prod[threadIdx.x] = 0;
+        cons[threadIdx.x] = 0;
+    }
+    __syncthreads();
+    const unsigned wmask = (unsigned)kp.wrap_rows - 1u;
+    // progress words: lane 0 writes the word, the others a sink (no exec-mask branch)
+    int* const prod_out = lane == 0 ? &prod[wave] : &psink[wave][lane];
+    int* const cons_out = lane == 0 ? &cons[wave] : &psink[wave][lane];
+    int base = 0, prev = 0;   // position bases of this round and the last
+    for (int di = blockIdx.x; di < kp.npairs; di += gridDim.x) {
+        const DuoDesc d = load_duo(kp, di);
+        const int span = (d.m_pad + 64 * W - 1 + C - 1) / C * C + 128;
+        for (int r = 0; 4 * r < d.strips; ++r) {
+            const int strip = 4 * r + wave;
+            if (strip < d.strips) {
+                const DuoLink<LIN> in{wave > 0 ? ring[wave - 1] : wrap, wave > 0 ? (unsigned)DUO_R - 1u : wmask,
+                                      wave > 0 ? base : 0, wave > 0 ? base : prev, &prod[(wave + 3) & 3], nullptr};
+                const DuoLink<LIN> out{wave < 3 ? ring[wave] : wrap, wave < 3 ? (unsigned)DUO_R - 1u : wmask,
+                                       wave < 3 ? base : 0, base, nullptr, wave < 3 ? &cons[wave + 1] : nullptr};
+                strip_pass_duo_lds<W, C, M3, LIN>(kp, d, strip, lane, strip > 0, in, strip + 1 < d.strips, out,
+                                                  prod_out, cons_out, sink[wave]);
+            }
+            prev = base;
+            base += span;
+        }
+    }
+}
+
 template <class K>
-int occupancy_waves(K kernel, int threads = 256) {
+int occupancy_waves(K kernel, int threads = 256, int dyn = 0) {
     int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)kernel, threads, 0) != hipSuccess) return 4;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)kernel, threads, dyn) != hipSuccess) return 4;
     return nb * threads / 64;
 }
 
@@ -964,6 +1132,22 @@ hipError_t launch_t(const LaunchCfg& cfg, const KParams& kp, hipStream_t s) {
             }
             return hipErrorInvalidValue;
         case MODE_DUO:
+            if constexpr (DNA && C == 64) {
+                if (cfg.duo_wrap > 0) {   // every hand-off in LDS
+                    const int dyn = cfg.duo_wrap * (cfg.f2_lin ? 4 : 8);
+                    if (dyn > DUO_LDS_DYN_MAX) return hipErrorInvalidValue;
+                    auto go = [&](auto kern) -> hipError_t {
+                        // the wrap buffer and the static rings may pass 64 KB together
+                        const hipError_t e = raise_dyn_lds((const void*)kern, DUO_LDS_DYN_MAX);
+                        if (e != hipSuccess) return e;
+                        hipLaunchKernelGGL(kern, dim3(cfg.blocks), dim3(64 * DUO_WAVES), (size_t)dyn, s, kp);
+                        return hipGetLastError();
+                    };
+                    if (cfg.duo_f16 && cfg.f2_lin) return go(sw_duo_lds_kernel<W, C, true, true>);
+                    if (cfg.duo_f16) return go(sw_duo_lds_kernel<W, C, true, false>);
+                    return go(sw_duo_lds_kernel<W, C, false, false>);
+                }
+            }
             if constexpr (DNA) {
                 // the linear-gap step (G_INIT == G_EXT) is built with the f16-max3 form
                 if (cfg.duo_f16 && cfg.f2_lin)
@@ -981,7 +1165,16 @@ hipError_t launch_t(const LaunchCfg& cfg, const KParams& kp, hipStream_t s) {
 }
 
 template <int W, int C, bool DNA>
-int waves_t(int mode) {
+int waves_t(const LaunchCfg& cfg) {
+    const int mode = cfg.mode;
+    if constexpr (DNA && C == 64) {
+        if (mode == MODE_DUO && cfg.duo_wrap > 0) {
+            const int dyn = cfg.duo_wrap * (cfg.f2_lin ? 4 : 8);
+            return cfg.f2_lin    ? occupancy_waves(sw_duo_lds_kernel<W, C, true, true>, 64 * DUO_WAVES, dyn)
+                   : cfg.duo_f16 ? occupancy_waves(sw_duo_lds_kernel<W, C, true, false>, 64 * DUO_WAVES, dyn)
+                                 : occupancy_waves(sw_duo_lds_kernel<W, C, false, false>, 64 * DUO_WAVES, dyn);
+        }
+    }
     switch (mode) {
         case MODE_STRIP: return occupancy_waves(sw_strip_kernel<W, C, DNA>);
         case MODE_PAIRWG: return occupancy_waves(sw_pairwg_kernel<W, C, DNA>);
@@ -1018,7 +1211,7 @@ hipError_t launch_sw_strip(const LaunchCfg& cfg, const KParams& kp, hipStream_t 
 
 int kernel_waves_per_cu(const LaunchCfg& cfg) {
 #define SW_OCC(w, c) \
-    if (cfg.W == w && cfg.C == c) return cfg.dna ? waves_t<w, c, true>(cfg.mode) : waves_t<w, c, false>(cfg.mode);
+    if (cfg.W == w && cfg.C == c) return cfg.dna ? waves_t<w, c, true>(cfg) : waves_t<w, c, false>(cfg);
     SW_VARIANTS(SW_OCC)
 #undef SW_OCC
     return 4;

@@ -192,6 +192,10 @@ void sw_db_close(sw_db* db);
  *   "f3"       1 = (default) a two-column linear-gap flow2 launch runs the flow3 kernel
  *              (hand-scheduled chunk loops): staged codes at C = 32 / 16 (C2), ring edges at
  *              C = 64 (C5); 0 = the compiled flow2 kernel
+ *   "duo_lds"  1 = (default) duo batches at C = 64 hand strip edges on in LDS when a round's
+ *              rows fit (m <= 16384 linear-gap step, 8192 affine), 0 = through HBM granules
+ *   "duo_rev"  1 = the duo LDS kernel's odd workgroups run the strip roles in reverse wave
+ *              order (SIMD balance of the pipeline fill), 0 = (default) the same order
  *   "slab_plain" 1 = an exported slab buffer may fall back to plain device memory (one-GPU
  *              tests only; cross-GPU edges need fine-grained memory), 0 = (default) refuse
  *   "trace"    device address of a 16 x u64 per-strip trace buffer, 0 = off (tools)
@@ -210,7 +214,8 @@ typedef struct {
     int variant;            /* bit 0: duo max3 via v_pk_maximum3_f16; bit 1: flow2 streams row codes;
                                bit 2: flow2 ring edges; bit 3: the linear-gap step;
                                bit 4: flow2 two columns per lane; bit 5: flow2 pair per workgroup;
-                               bit 6: the flow3 kernel (sw_flow3.hip) */
+                               bit 6: the flow3 kernel (sw_flow3.hip);
+                               bit 7: duo strip hand-offs in LDS (no boundary buffers) */
 } sw_stats;
 int sw_last_stats(sw_stats* out);
 

@@ -1,0 +1,119 @@
+"""GPU parity of the duo kernel with every strip hand-off in LDS (sw_kernels.hip
+sw_duo_lds_kernel, option duo_lds, variant bit 128) against the oracle and against the
+granule duo kernel (duo_lds = 0) on the same inputs.  Bit-exact integer equality.
+
+Covered: strips per duo 1..7 (rounds with idle waves), rows around the 64-row chunk and
+the 511-step lane skew, ragged pairs padded inside a duo, the linear-gap and the affine
+step (4- and 8-byte slots), grids of 1-3 workgroups (many duos per workgroup, rounds
+crossing duos without a barrier), odd workgroups in reverse wave order (duo_rev), rows
+beyond the LDS wrap buffer (the granule kernel then), and C3 in full against its golden."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ACGT = np.frombuffer(b"ACGT", np.uint8)
+
+
+def _rand_dna(rng, n):
+    return ACGT[rng.integers(0, 4, n)]
+
+
+def _related(rng, n, m, p=0.1):
+    a = _rand_dna(rng, n)
+    b = np.resize(a, m).copy()
+    mut = rng.random(m) < p
+    b[mut] = _rand_dna(rng, int(mut.sum()))
+    return a, b
+
+
+@pytest.fixture(autouse=True)
+def _defaults(engine):
+    yield
+    for k in ("blocks", "W", "C"):
+        engine.set_option(k, 0)
+    engine.set_option("mode", -1)
+    engine.set_option("duo_lds", 1)
+    engine.set_option("duo_rev", 0)
+    engine.set_option("linear", -1)
+
+
+def _check(engine, oracle_mod, pairs, prm, lds_expected=True):
+    op = oracle_mod.Params(prm.match, prm.mismatch, prm.gap_init, prm.gap_ext)
+    exp = [oracle_mod.score_linear(a, b, op) for a, b in pairs]
+    engine.set_option("mode", 3)
+    engine.set_option("duo_lds", 1)
+    got = engine.score_batch(pairs, prm)
+    st = engine.last_stats()
+    assert st["mode"] == 3, st
+    assert bool(st["variant"] & 128) == lds_expected, st
+    if lds_expected:
+        assert st["boundary_bytes"] == 0, st
+    assert got == exp, ("lds", prm)
+    engine.set_option("duo_lds", 0)
+    assert engine.score_batch(pairs, prm) == exp, ("granules", prm)
+    assert not engine.last_stats()["variant"] & 128
+    engine.set_option("duo_lds", 1)
+    return exp
+
+
+PARAMS = [(1, -1, 1, 1), (2, -3, 5, 2), (3, -1, 4, 1), (3, -2, 5, 5)]
+
+
+@pytest.mark.parametrize("prm_t", PARAMS)
+def test_duo_lds_strip_counts_and_rows(engine, oracle_mod, prm_t):
+    """Duos of 1..7 strips (W = 8: 512 columns each; rounds with 1-3 idle waves) and rows
+    around the chunk and the lane skew, as ragged pairs; the linear-gap and affine steps."""
+    prm = engine.Params(*prm_t)
+    rng = np.random.default_rng(1000 + sum(prm_t))
+    ns = [100, 512, 513, 1100, 1600, 2048, 2100, 2700, 3500]
+    ms = [1, 2, 63, 64, 65, 511, 512, 513, 575, 1000, 2049]
+    pairs = []
+    for i in range(14):
+        n, m = ns[i % len(ns)], ms[(3 * i) % len(ms)]
+        pairs.append(_related(rng, n, m) if i % 3 else (_rand_dna(rng, n), _rand_dna(rng, m)))
+    for lin in ((-1, 0) if prm.gap_init == prm.gap_ext else (-1,)):
+        engine.set_option("linear", lin)
+        _check(engine, oracle_mod, pairs, prm)
+
+
+def test_duo_lds_grids_and_reverse_roles(engine, oracle_mod):
+    """11 duos on grids of 1, 2 and 3 workgroups (a workgroup's waves run from one duo into
+    the next with no barrier, positions continuing across rounds and duos), with the strip
+    roles in reverse wave order on odd workgroups and without."""
+    rng = np.random.default_rng(9)
+    pairs = [_related(rng, int(rng.integers(300, 4200)), int(rng.integers(50, 3000))) for _ in range(22)]
+    for prm in (engine.Params(), engine.Params(2, -3, 5, 2)):
+        for rev in (0, 1):
+            engine.set_option("duo_rev", rev)
+            for blocks in (1, 2, 3):
+                engine.set_option("blocks", blocks)
+                _check(engine, oracle_mod, pairs, prm)
+    engine.set_option("blocks", 0)
+
+
+def test_duo_lds_wrap_buffer_limit(engine, oracle_mod):
+    """The wrap buffer holds a round's rows in at most 64 KB of LDS: m_pad <= 16384 at the
+    linear-gap step (4-byte slots), <= 8192 affine (8 bytes); longer rows take the granule
+    kernel, with the same scores."""
+    rng = np.random.default_rng(4)
+    for prm, m_ok, m_over in ((1, 16384, 16385), (0, 8192, 8193)):
+        p = engine.Params() if prm else engine.Params(2, -3, 5, 2)
+        for m, lds in ((m_ok, True), (m_over, False)):
+            pairs = [_related(rng, 700, m), _related(rng, 1300, m - 7), (_rand_dna(rng, 90), _rand_dna(rng, 40))]
+            _check(engine, oracle_mod, pairs, p, lds_expected=lds)
+
+
+def test_duo_lds_c3_golden(engine, golden):
+    """C3 (1024 pairs N = 8192, the reference-pinned golden) on the LDS duo kernel, in both
+    wave orders; no strip-boundary buffer in HBM."""
+    c = golden("configs.json")["C3"]
+    N = c["N"]
+    arena = engine.gen_batch(c["seed_base"], c["npairs"], N)
+    pairs = [(arena[2 * N * k:2 * N * k + N], arena[2 * N * k + N:2 * N * (k + 1)]) for k in range(c["npairs"])]
+    for rev in (0, 1):
+        engine.set_option("duo_rev", rev)
+        got = engine.score_batch(pairs)
+        st = engine.last_stats()
+        assert st["mode"] == 3 and st["variant"] & 128 and st["boundary_bytes"] == 0, st
+        assert got == c["scores"], rev
