@@ -687,7 +687,9 @@ def main():
     value = cells_job * args.steps / t_max / 1e9
     if rank == 0:
         out = {
-            "metric": "GCUPS (cell updates/s) for NxN affine-gap SW; bit-exact score vs CPU",
+            "metric": "GCUPS (cell updates/s) for NxN affine-gap SW; bit-exact score vs CPU"
+                      + ("; N>1: one C2-size pair per GPU (the batched pairs: batch_c4)"
+                         if world > 1 and workload == "pair" else ""),
             "value": round(value, 3),
             "unit": "GCUPS",
             "n_gpus": world,

@@ -99,10 +99,11 @@ def kernel_mix(path, filt):
     for name, body in _kernels(path):
         if filt not in name:
             continue
-        labels = {m.group(1): i for i, l in enumerate(body) for m in [re.match(r"^(\.LBB\S+):", l)] if m}
+        # compiler blocks (.LBB...) and the labels of hand-written asm loops (flow3: L_loop_<n>)
+        labels = {m.group(1): i for i, l in enumerate(body) for m in [re.match(r"^\s*(\.LBB\S+|L_\w+):", l)] if m}
         loops = []
         for i, l in enumerate(body):
-            m = re.match(r"^\s+s_c?branch\w*\s+(\.LBB\S+)", l)
+            m = re.match(r"^\s+s_c?branch\w*\s+(\.LBB\S+|L_\w+)", l)
             if not m or m.group(1) not in labels or labels[m.group(1)] >= i:
                 continue
             ops = [x.split()[0] for x in body[labels[m.group(1)]:i + 1] if re.match(r"^\s+[vsdgb][a-z_0-9]+", x)]

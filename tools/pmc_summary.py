@@ -4,7 +4,8 @@ profile summaries.
 
     python tools/pmc_summary.py gpurun_out/prof r02
 
-For each workload (c2 -> pair, c3 -> batch, c5 -> slab on one GPU):
+For each workload (c2 -> pair, c3 -> batch, c5 -> slab on one GPU, c5p8 -> slab_part: slab 0 of
+C5's 8-way column split alone):
   * copies the kernel-trace stats, the counter CSVs and the bench line to
     profiles/<round>_<cfg>_*;
   * writes profiles/pmc_<workload>.json, which bench.py reads for its roofline,
@@ -37,7 +38,17 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ALGO_BYTES_PER_CELL = 12
 CELLS = {"c2": 65536 * 65536, "c3": 1024 * 8192 * 8192, "c5": (1 << 20) * (1 << 20)}
-WORKLOAD = {"c2": "pair", "c3": "batch", "c5": "slab"}
+WORKLOAD = {"c2": "pair", "c3": "batch", "c5": "slab", "c5p8": "slab_part"}
+
+
+def cells(cfg):
+    """Cells per launch; c5p8: slab 0 of the 8-way column split of C5 alone (bench.py --slab-of 8)."""
+    if cfg == "c5p8":
+        sys.path.insert(0, ROOT)
+        import concurrentproject_amd as sw
+        b = sw.slab_bounds(1 << 20, 1 << 20, 8, sw.SW_FLAG_DNA)
+        return (b[1] - b[0]) * (1 << 20)
+    return CELLS[cfg]
 LIB = os.path.join(ROOT, "concurrentproject_amd", "libswmi355.so")
 
 
@@ -80,10 +91,12 @@ def valu_mix(kernel):
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     import issue_model
     csrc = os.path.join(ROOT, "concurrentproject_amd", "csrc")
-    base = "sw_flow2" if "sw_flow2_kernel" in kernel else "sw_kernels"
+    base = "sw_flow3" if "sw_flow3" in kernel else "sw_flow2" if "sw_flow2_kernel" in kernel else "sw_kernels"
     out = os.path.join(ROOT, "build", "asm")
     s_path = os.path.join(out, base + "-hip-amdgcn-amd-amdhsa-gfx950.s")
     deps = [os.path.join(csrc, f) for f in (base + ".hip", "sw_device.h", "sw_internal.h")]
+    if base == "sw_flow3":
+        deps += [os.path.join(csrc, f) for f in ("sw_flow3_loops.inc", "sw_flow3r_loops.inc")]
     if not os.path.exists(s_path) or os.path.getmtime(s_path) < max(os.path.getmtime(d) for d in deps):
         os.makedirs(out, exist_ok=True)
         subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-c",
@@ -114,7 +127,7 @@ def main():
         return mix_only()
     src, rnd = sys.argv[1], sys.argv[2]
     prof = os.path.join(ROOT, "profiles")
-    for cfg in ("c2", "c3", "c5"):
+    for cfg in ("c2", "c3", "c5", "c5p8"):
         stats = os.path.join(src, "kt_" + cfg, cfg + "_kernel_stats.csv")
         if not os.path.exists(stats):
             print("skip", cfg)
@@ -132,7 +145,7 @@ def main():
         t_ns = float(st["AverageNs"])
         out = {"kernel": k, "lib_sha256": sha256(LIB), "source_sha256": source_stamp(), "kernel_avg_ns": t_ns,
                "kernel_calls": int(st["Calls"]),
-               "algorithmic_bytes_per_launch": CELLS[cfg] * ALGO_BYTES_PER_CELL, "cells_per_launch": CELLS[cfg]}
+               "algorithmic_bytes_per_launch": cells(cfg) * ALGO_BYTES_PER_CELL, "cells_per_launch": cells(cfg)}
         passes = []
         fetch = os.path.join(src, "fetch_" + cfg, cfg + "_counter_collection.csv")
         write = os.path.join(src, "write_" + cfg, cfg + "_counter_collection.csv")
@@ -157,7 +170,7 @@ def main():
             out["valu_insts_per_launch"] = out.get("SQ_INSTS_VALU")
             out["valu_lane_ops_per_launch"] = out["valu_insts_per_launch"] * 64
             out["valu_frac_at_2p4ghz"] = out["valu_lane_ops_per_launch"] / (t_ns * 1e-9) / (256 * 4 * 32 * 2.4e9)
-            out["valu_insts_per_cell"] = out["valu_insts_per_launch"] / CELLS[cfg]
+            out["valu_insts_per_cell"] = out["valu_insts_per_launch"] / cells(cfg)
             passes.append(" ".join(names))
         grbm = os.path.join(src, "grbm_" + cfg, cfg + "_counter_collection.csv")
         if os.path.exists(grbm):

@@ -4,7 +4,7 @@ set -e
 # PMC slots) for C2 (pair), C3 (batch) and C5 (slab workload, 1 GPU):
 #   FETCH_SIZE | WRITE_SIZE | SQ (8 slots) | GRBM
 # then python tools/pmc_summary.py gpurun_out/prof <round> (in the build container).
-# usage (on the GPU box): bash tools/prof_round.sh [c2 c3 c5]
+# usage (on the GPU box): bash tools/prof_round.sh [c2 c3 c5 c5p8]
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out/prof
 which="${*:-c2 c3 c5}"
@@ -14,6 +14,7 @@ for w in $which; do
     c2) args="--steps 10 --warmup 2"; pargs="--workload pair --steps 5 --warmup 1";;
     c3) args="--workload batch --steps 5 --warmup 1"; pargs="--workload batch --steps 3 --warmup 1";;
     c5) args="--workload slab --steps 3 --warmup 1 --cpu-seconds 10"; pargs="--workload slab --steps 2 --warmup 1";;
+    c5p8) args="--workload slab --slab-of 8 --steps 3 --warmup 1 --no-cpu-baseline"; pargs="--workload slab --slab-of 8 --steps 2 --warmup 1";;
   esac
   timeout -k 10 240 python bench.py $args > gpurun_out/prof/bench_$w.json 2> gpurun_out/prof/bench_$w.err
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof/kt_$w -o $w -- python bench.py $pargs --no-cpu-baseline > gpurun_out/prof/kt_$w.log 2>&1
