@@ -448,6 +448,11 @@ int finalize_mode(Job& job, const Params& prm, int cus) {
             // ring mode (one pair of many groups per CU, C5): throughput-bound, so 64-row chunks
             // (half the per-chunk work per step) beat the shorter hand-off lag of 32 (C5 249 -> 220 ms)
             if (job.ring && g_opt_C.load() == 0) job.C = 64;
+            // the staged two-column kernel on flow3 (C2): 16-row chunks, whose shorter hand-off lag
+            // (63 + 16 steps a strip) outweighs their per-chunk work there (2.70 -> 2.65 ms)
+            if (!job.ring && !job.f2_stream && job.f2w2 && g_opt_C.load() == 0 && g_opt_f3.load() != 0 &&
+                flow3_fits(max_m, 16))
+                job.C = 16;
             return 0;
         }
         if (job.mode == MODE_FLOW2) {

@@ -1100,6 +1100,11 @@ __global__ void __launch_bounds__(64 * DUO_WAVES) sw_duo_lds_kernel(KParams kp) 
                 strip_pass_duo_lds<W, C, M3, LIN>(kp, d, strip, lane, strip > 0, in, strip + 1 < d.strips, out,
                                                   prod_out, cons_out, sink[wave]);
             }
+            // done with every position before the next round, read or not: a producer's back-pressure
+            // must not wait on a consumer that skipped rounds (idle waves of a duo's last round) --
+            // its word would stay below the producer's floor (found by a protocol simulation)
+            compiler_fence();
+            *cons_out = base + span;
             prev = base;
             base += span;
         }

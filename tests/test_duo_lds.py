@@ -38,14 +38,17 @@ def _defaults(engine):
     engine.set_option("linear", -1)
 
 
-def _check(engine, oracle_mod, pairs, prm, lds_expected=True):
+def _check(engine, oracle_mod, pairs, prm, lds_expected=True, W=8):
+    """The duo kernel at W columns per lane and 64-row chunks (the LDS links' chunk)."""
     op = oracle_mod.Params(prm.match, prm.mismatch, prm.gap_init, prm.gap_ext)
     exp = [oracle_mod.score_linear(a, b, op) for a, b in pairs]
     engine.set_option("mode", 3)
+    engine.set_option("W", W)
+    engine.set_option("C", 64)
     engine.set_option("duo_lds", 1)
     got = engine.score_batch(pairs, prm)
     st = engine.last_stats()
-    assert st["mode"] == 3, st
+    assert st["mode"] == 3 and st["W"] == W and st["C"] == 64, st
     assert bool(st["variant"] & 128) == lds_expected, st
     if lds_expected:
         assert st["boundary_bytes"] == 0, st
@@ -62,7 +65,7 @@ PARAMS = [(1, -1, 1, 1), (2, -3, 5, 2), (3, -1, 4, 1), (3, -2, 5, 5)]
 
 @pytest.mark.parametrize("prm_t", PARAMS)
 def test_duo_lds_strip_counts_and_rows(engine, oracle_mod, prm_t):
-    """Duos of 1..7 strips (W = 8: 512 columns each; rounds with 1-3 idle waves) and rows
+    """Duos of 1..7 strips (W = 8: 512 columns each, W = 4: 256; rounds with 1-3 idle waves) and rows
     around the chunk and the lane skew, as ragged pairs; the linear-gap and affine steps."""
     prm = engine.Params(*prm_t)
     rng = np.random.default_rng(1000 + sum(prm_t))
@@ -74,7 +77,8 @@ def test_duo_lds_strip_counts_and_rows(engine, oracle_mod, prm_t):
         pairs.append(_related(rng, n, m) if i % 3 else (_rand_dna(rng, n), _rand_dna(rng, m)))
     for lin in ((-1, 0) if prm.gap_init == prm.gap_ext else (-1,)):
         engine.set_option("linear", lin)
-        _check(engine, oracle_mod, pairs, prm)
+        for W in (8, 4):
+            _check(engine, oracle_mod, pairs, prm, W=W)
 
 
 def test_duo_lds_grids_and_reverse_roles(engine, oracle_mod):
