@@ -1087,6 +1087,8 @@ __global__ void __launch_bounds__(64 * DUO_WAVES) sw_duo_lds_kernel(KParams kp) 
     int* const prod_out = lane == 0 ? &prod[wave] : &psink[wave][lane];
     int* const cons_out = lane == 0 ? &cons[wave] : &psink[wave][lane];
     int base = 0, prev = 0;   // position bases of this round and the last
+    // tools/probe_duo_simd.py: where each wave runs (HW_ID: SIMD, CU, SE; XCC_ID) and when
+    const unsigned long long t_begin = kp.trace != nullptr ? __builtin_amdgcn_s_memrealtime() : 0ull;
     for (int di = blockIdx.x; di < kp.npairs; di += gridDim.x) {
         const DuoDesc d = load_duo(kp, di);
         const int span = (d.m_pad + 64 * W - 1 + C - 1) / C * C + 128;
@@ -1108,6 +1110,14 @@ __global__ void __launch_bounds__(64 * DUO_WAVES) sw_duo_lds_kernel(KParams kp) 
             prev = base;
             base += span;
         }
+    }
+    if (kp.trace != nullptr && lane == 0) {
+        unsigned long long* t = kp.trace + 4ull * (4u * blockIdx.x + (unsigned)hw);
+        // HW_REG_HW_ID, and the strip role this wave ran at bit 40
+        t[0] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4) | ((unsigned long long)wave << 40);
+        t[1] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20);   // HW_REG_XCC_ID
+        t[2] = t_begin;
+        t[3] = __builtin_amdgcn_s_memrealtime();
     }
 }
 

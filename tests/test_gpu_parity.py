@@ -209,9 +209,10 @@ def test_flow2_ragged(engine, oracle_mod):
             engine.set_option("mode", 5)
             for C in (16, 32, 64):
                 engine.set_option("C", C)
-                # G_INIT == G_EXT at C = 32 / 64: the linear-gap step (auto) at two columns per lane (auto)
-                # and at one (f2w = 1), and the affine step (linear = 0)
-                lin_ok = prm.gap_init == prm.gap_ext and C in (32, 64)
+                # G_INIT == G_EXT: the linear-gap step (auto) at two columns per lane (auto) and, at
+                # C = 32 / 64, at one (f2w = 1); the affine step (linear = 0).  C = 16 has the linear
+                # step only at two columns per lane (the flow3 kernel)
+                lin_ok = prm.gap_init == prm.gap_ext
                 for lin, f2w in (((-1, 0), (-1, 1), (0, 0)) if lin_ok else ((-1, 0),)):
                     engine.set_option("linear", lin)
                     engine.set_option("f2w", f2w)
@@ -219,8 +220,9 @@ def test_flow2_ragged(engine, oracle_mod):
                     assert got == exp, (C, prm, lin, f2w)
                     st = engine.last_stats()
                     assert st["mode"] == 5
-                    assert bool(st["variant"] & 8) == (lin == -1 and lin_ok), st
-                    assert bool(st["variant"] & 16) == (lin == -1 and lin_ok and f2w == 0), st
+                    lin_step = lin == -1 and lin_ok and (C != 16 or f2w == 0)
+                    assert bool(st["variant"] & 8) == lin_step, st
+                    assert bool(st["variant"] & 16) == (lin_step and f2w == 0), st
                     assert engine.score_batch(pairs, prm) == exp, (C, prm, lin, f2w)
                 engine.set_option("linear", -1)
                 engine.set_option("f2w", 0)
