@@ -192,6 +192,7 @@ struct Job {
     std::vector<int> item_base;
     long long cells = 0;
     uint64_t bnd_granules = 0;
+    bool slab = false;           // a column slab (sw_score_slab_device): flow2 streams its rows
     int W = 1, C = 16;
     int mode = MODE_STRIP;
     bool dna = true;
@@ -351,8 +352,11 @@ bool flow2_staged(const Job& job, int max_m) {
 // of 5.5 VALU per 64 cells, throughput-bound).
 bool flow2_w2_wanted(const Job& job, const Params& p) {
     const long long o = g_opt_f2w.load();
-    // (C = 16: flow3's staged kernel only, sw_flow3.hip; flow2 has no such two-column variant)
-    const bool c16 = g_opt_f3.load() != 0;
+    // (C = 16: flow3's staged kernel only, sw_flow3.hip; flow2 has no such two-column variant,
+    // so streamed rows at C = 16 keep one column per lane)
+    int max_m = 0;
+    for (const PairDesc& d : job.pairs) max_m = std::max(max_m, d.m);
+    const bool c16 = g_opt_f3.load() != 0 && !job.slab && flow2_staged(job, max_m) && flow3_fits(max_m, 16);
     const bool lin = p.gap_init == p.gap_ext && g_opt_linear.load() != 0 && (job.C != 16 || c16) &&
                      (g_opt_C.load() == 0 || g_opt_C.load() == 32 || g_opt_C.load() == 64 ||
                       (g_opt_C.load() == 16 && c16));
@@ -450,7 +454,7 @@ int finalize_mode(Job& job, const Params& prm, int cus) {
             if (job.ring && g_opt_C.load() == 0) job.C = 64;
             // the staged two-column kernel on flow3 (C2): 16-row chunks, whose shorter hand-off lag
             // (63 + 16 steps a strip) outweighs their per-chunk work there (2.70 -> 2.65 ms)
-            if (!job.ring && !job.f2_stream && job.f2w2 && g_opt_C.load() == 0 && g_opt_f3.load() != 0 &&
+            if (!job.ring && !job.f2_stream && !job.slab && job.f2w2 && g_opt_C.load() == 0 && g_opt_f3.load() != 0 &&
                 flow3_fits(max_m, 16))
                 job.C = 16;
             return 0;
@@ -535,6 +539,7 @@ int plan_slab(Job& job, int n, int m, bool dna, const Params& prm) {
     d.m = m;
     d.out_idx = 0;
     job.dna = dna;
+    job.slab = true;
     const long long fw = g_opt_W.load();
     const int W = fw ? (int)fw : 1;
     const long long fm = g_opt_mode.load();
@@ -653,13 +658,13 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
                                    (job.mode == MODE_DUO && job.duo_f16)) &&
                                       prm.gap_init == prm.gap_ext && g_opt_linear.load() != 0;
     // flow3 (sw_flow3.hip, hand-scheduled chunk loops) for the two-column linear-gap launches it
-    // implements: the staged single-pair kernel (C = 32, rows in LDS: C2) and ring mode (C = 64,
-    // streamed rows, one pair: C5); option f3 = 0 keeps flow2
+    // implements: the staged single-pair kernel (C = 16 / 32, rows in LDS: C2) and ring mode (C = 64
+    // / 32, streamed rows, one pair: C5); option f3 = 0 keeps flow2
     int max_m_f3 = 0;
     for (const PairDesc& d : job.pairs) max_m_f3 = std::max(max_m_f3, d.m);
     const bool f3_base = g_opt_f3.load() != 0 && job.mode == MODE_FLOW2 && job.f2w2 && f2_lin && !job.pwg;
     const bool use_f3 = f3_base && ((!f2s && !job.ring && flow3_fits(max_m_f3, job.C)) ||
-                                    (job.ring && edge == nullptr && job.C == 64));
+                                    (job.ring && edge == nullptr && (job.C == 64 || job.C == 32)));
     // duo batches at C = 64: strip hand-offs in LDS when the wrap buffer (a round's rows of
     // both pairs) fits the default dynamic-LDS limit; no boundary buffers in HBM then
     int duo_wrap = 0;
@@ -1615,7 +1620,7 @@ int sw_set_option(const char* key, long long v) {
     } else if (k == "duo_lds") {   // 1 (default): duo strip hand-offs in LDS when the wrap buffer fits, 0: HBM granules
         if (v < 0 || v > 1) return -1;
         g_opt_duo_lds = v;
-    } else if (k == "duo_rev") {   // 1: the duo LDS kernel's odd workgroups run the strip roles in reverse wave order
+    } else if (k == "duo_rev") {   // 1: the duo LDS kernel assigns strip roles by SIMD (complementary per CU)
         if (v < 0 || v > 1) return -1;
         g_opt_duo_rev = v;
     } else if (k == "slab_plain") {   // 1: exported slab buffers may fall back to plain device memory

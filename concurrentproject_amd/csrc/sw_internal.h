@@ -97,7 +97,7 @@ struct KParams {
     int wrap_rows;
     unsigned* ring_cons;          // ring j's consumer progress (positions consumed), RING_CONS_STRIDE apart
     // (the duo kernel with LDS hand-offs takes its wrap-buffer slots from wrap_rows)
-    int duo_rev;                  // duo LDS kernel: odd workgroups map strip roles to waves in reverse
+    int duo_rev;                  // duo LDS kernel: strip roles by SIMD (complementary across a CU's workgroups)
 };
 
 constexpr int RING_CONS_STRIDE = 32;   // dwords between consumer progress words (one 128-B line each)

@@ -1064,7 +1064,7 @@ __device__ void strip_pass_duo_lds(const KParams& kp, const DuoDesc& d, const in
 }
 
 // kp.wrap_rows: slots of the wrap buffer (a power of two >= every duo's m_pad);
-// kp.duo_rev: odd workgroups run the strip roles in reverse wave order (see LaunchCfg)
+// kp.duo_rev: strip roles by SIMD (complementary on the two workgroups of a CU), else by wave index
 template <int W, int C, bool M3, bool LIN>
 __global__ void __launch_bounds__(64 * DUO_WAVES) sw_duo_lds_kernel(KParams kp) {
     static_assert(DUO_WAVES == 4, "the LDS links pair waves w -> w + 1 and 3 -> 0");
@@ -1074,14 +1074,30 @@ __global__ void __launch_bounds__(64 * DUO_WAVES) sw_duo_lds_kernel(KParams kp) 
     __shared__ Slot ring[3][DUO_R];
     __shared__ Slot sink[4][64];
     __shared__ int prod[4], cons[4], psink[4][64];
+    __shared__ int s_simd[4];
     const int lane = threadIdx.x & 63;
     const int hw = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    const int wave = kp.duo_rev && (blockIdx.x & 1) ? 3 - hw : hw;
+    // the SIMD this wave runs on (HW_REG_HW_ID bits 5:4)
+    const int my_simd = __builtin_amdgcn_readfirstlane((int)((__builtin_amdgcn_s_getreg((31 << 11) | 4) >> 4) & 3));
     if (threadIdx.x < 4) {
         prod[threadIdx.x] = 0;
         cons[threadIdx.x] = 0;
     }
+    if (lane == 0) s_simd[hw] = my_simd;
     __syncthreads();
+    // strip roles: wave index, or (kp.duo_rev) by SIMD so that the two workgroups sharing a CU
+    // hold complementary roles on each SIMD (r and 3 - r: one starts its strips late where the
+    // other starts early).  The dispatcher places a workgroup's waves on consecutive SIMDs from
+    // the one wave 0 got (observed: 0 for one workgroup of a CU, 1 for the other); roles follow
+    // the SIMD, mirrored when wave 0's SIMD is odd -- only if the 4 SIMDs are distinct, so the
+    // roles are always a permutation of the waves (placement affects speed, never results)
+    int wave = hw;
+    if (kp.duo_rev) {
+        const int s0 = s_simd[0];
+        if (((1 << s0) | (1 << s_simd[1]) | (1 << s_simd[2]) | (1 << s_simd[3])) == 15)
+            wave = (s0 & 1) ? 3 - my_simd : my_simd;
+    }
+    wave = __builtin_amdgcn_readfirstlane(wave);
     const unsigned wmask = (unsigned)kp.wrap_rows - 1u;
     // progress words: lane 0 writes the word, the others a sink (no exec-mask branch)
     int* const prod_out = lane == 0 ? &prod[wave] : &psink[wave][lane];

@@ -194,8 +194,8 @@ void sw_db_close(sw_db* db);
  *              C = 64 (C5); 0 = the compiled flow2 kernel
  *   "duo_lds"  1 = (default) duo batches at C = 64 hand strip edges on in LDS when a round's
  *              rows fit (m <= 16384 linear-gap step, 8192 affine), 0 = through HBM granules
- *   "duo_rev"  1 = the duo LDS kernel's odd workgroups run the strip roles in reverse wave
- *              order (SIMD balance of the pipeline fill), 0 = (default) the same order
+ *   "duo_rev"  1 = the duo LDS kernel assigns strip roles by SIMD, so the two workgroups of a
+ *              CU hold complementary roles on each SIMD (pipeline fill), 0 = by wave index
  *   "slab_plain" 1 = an exported slab buffer may fall back to plain device memory (one-GPU
  *              tests only; cross-GPU edges need fine-grained memory), 0 = (default) refuse
  *   "trace"    device address of a 16 x u64 per-strip trace buffer, 0 = off (tools)

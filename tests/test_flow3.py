@@ -126,7 +126,7 @@ def test_flow3_config_c2(engine, golden):
 
 
 # ---- ring mode (sw_flow3.hip sw_flow3r_kernel: streamed row codes, group edges through
-# per-block rings, C = 64; the C5 organisation)
+# per-block rings, C = 64 or 32; the C5 organisation)
 
 def _ring_opts(engine, blocks, rows):
     engine.set_option("ring", 1)
@@ -152,16 +152,19 @@ def test_flow3_ring_parity(engine, oracle_mod, _ring_reset):
     for prm in (engine.Params(), engine.Params(2, -3, 4, 4), engine.Params(1, 0, 0, 0)):
         op = oracle_mod.Params(prm.match, prm.mismatch, prm.gap_init, prm.gap_ext)
         exp = [oracle_mod.score_linear(a, b, op) for a, b in pairs]
-        for blocks, rows in ((0, 4096), (1, 512), (2, 512), (3, 1024), (7, 512)):
-            _ring_opts(engine, blocks, rows)
-            got = []
-            for a, b in pairs:
-                got.append(engine.score(a, b, prm))
-                st = engine.last_stats()
-                groups = (((len(a) - 2 + 125) // 126 if len(a) > 128 else 1) + 3) // 4
-                if groups > 1:
-                    assert st["variant"] & 64 and st["variant"] & 4 and st["C"] == 64, st
-            assert got == exp, (prm, blocks, rows)
+        for C in (64, 32):   # 64-row chunks (automatic in ring mode) and 32 (option C)
+            engine.set_option("C", 0 if C == 64 else C)
+            for blocks, rows in ((0, 4096), (1, 512), (2, 512), (3, 1024), (7, 512)):
+                _ring_opts(engine, blocks, rows)
+                got = []
+                for a, b in pairs:
+                    got.append(engine.score(a, b, prm))
+                    st = engine.last_stats()
+                    groups = (((len(a) - 2 + 125) // 126 if len(a) > 128 else 1) + 3) // 4
+                    if groups > 1:
+                        assert st["variant"] & 64 and st["variant"] & 4 and st["C"] == C, st
+                assert got == exp, (prm, C, blocks, rows)
+        engine.set_option("C", 0)
 
 
 def test_flow3_ring_matches_flow2(engine, _ring_reset):
@@ -174,12 +177,17 @@ def test_flow3_ring_matches_flow2(engine, _ring_reset):
     s = torch.cuda.current_stream()
     engine.set_option("ring", 1)
     out = []
-    for f3 in (1, 0):
-        engine.set_option("f3", f3)
-        engine.score_batch_device(arena.data_ptr(), [0], [N], [N], [N], score.data_ptr(), flags=1,
-                                  stream=s.cuda_stream)
-        engine.stream_status(s.cuda_stream)
-        st = engine.last_stats()
-        assert bool(st["variant"] & 64) == bool(f3) and st["variant"] & 4, st
-        out.append(score.item())
-    assert out[0] == out[1] > 0
+    try:
+        for f3, C in ((1, 0), (1, 32), (0, 0)):
+            engine.set_option("f3", f3)
+            engine.set_option("C", C)
+            engine.score_batch_device(arena.data_ptr(), [0], [N], [N], [N], score.data_ptr(), flags=1,
+                                      stream=s.cuda_stream)
+            engine.stream_status(s.cuda_stream)
+            st = engine.last_stats()
+            assert bool(st["variant"] & 64) == bool(f3) and st["variant"] & 4 and st["C"] == (C or 64), st
+            out.append(score.item())
+    finally:
+        engine.set_option("f3", 1)
+        engine.set_option("C", 0)
+    assert out[0] == out[1] == out[2] > 0

@@ -269,7 +269,7 @@ def emit(spec=0, halfpub=True):
 
 # ============================================================================================
 # Ring mode (C5: one pair N = 2^20, rows streamed, group edges through per-block rings):
-# sw_flow3.hip sw_flow3r_kernel, sw_flow3r_loops.inc.  C = 64, no loader wave, up to 4
+# sw_flow3.hip sw_flow3r_kernel, sw_flow3r_loops.inc.  C = 64 or 32, no loader wave, up to 4
 # workgroups per CU (the block's fixed registers stay below v108 so that 128 VGPRs suffice).
 #   v40/v41 IO / L0, v42..v50 step (RING below), v[52:67] / v[68:83] row codes of the even /
 #   odd chunk, v[84:85] granule inflow {H-G, key} (IN=GRAN) or LDS inflow row (v84), v86
@@ -305,9 +305,11 @@ def ring_granule(a):
     a("buffer_store_dwordx2 v[96:97], v99, %[gors], 0 offen sc1")
 
 
-def ring_gin_check(a):
-    """s[58:59] = live lanes (row k0 + lane < m); s[50:51] = live lanes whose granule fails."""
+def ring_gin_check(a, C=64):
+    """s[58:59] = live lanes (lane < C, row k0 + lane < m); s[50:51] = live lanes whose granule fails."""
     a("s_sub_i32 s54, %[m], s40")
+    if C < 64:
+        a(f"s_min_i32 s54, s54, {C}")
     a("v_cmp_gt_i32_e64 s[58:59], s54, %[lane]")
     a("v_xor_b32 v103, v84, v85")
     a("v_xor_b32 v103, v103, v102")
@@ -316,11 +318,14 @@ def ring_gin_check(a):
     a("s_cmp_lg_u64 s[50:51], 0")
 
 
-def gen_role_ring(IN, OUT_):
+def gen_role_ring(IN, OUT_, C=64):
+    """The ring-mode loop of one strip role at C-row chunks (64, or 32: half the hand-off
+    lag).  The loop body is two chunks; the code ring is refilled 64 rows per body."""
     L = []
     a = L.append
     lds_in, lds_out = IN == "lds", OUT_ == "lds"
     gin, gout = IN == "gran", OUT_ == "gran"
+    ncr = C // 16                                      # 16-B code reads per chunk
     # ---- entry (s_nop 4: descriptor operands may be fresh from v_readfirstlane)
     a("s_nop 4")
     a("s_waitcnt vmcnt(0) lgkmcnt(0)")
@@ -328,22 +333,25 @@ def gen_role_ring(IN, OUT_):
         a(f"v_mov_b32 {r}, 0")
     a("v_mov_b32 v40, %[ng]")
     a("v_mov_b32 v41, %[ng]")
-    a("v_mov_b32 v93, %[raw2]")                      # raw bytes of chunk 2 (loaded by the caller)
+    a("v_mov_b32 v93, %[raw2]")                      # raw bytes of rows 128..191 (loaded by the caller)
     a("v_mov_b32 v105, %[cro]")
     a("v_mov_b32 v106, %[rrow]")
     a("s_mov_b32 s40, 0")
-    a("s_mov_b32 s41, 0")
+    # LDS outflow slot base: C = 64 lanes 0..63 hold rows k0 - 128 + lane at slots k0 + lane; C = 32
+    # lanes 32..63 the new rows (slots k0 + lane, lane address (lane + 32) & 63 from base k0 + 32)
+    a(f"s_movk_i32 s41, {(64 - C) * 4:#x}")
     a("s_movk_i32 s42, 0x200")                       # ((0 + 128) mod R) * 4
-    a("s_movk_i32 s53, 0xc0")                        # slot base of chunk 2's codes: ((0 + 3) & 3) * 64
+    a("s_movk_i32 s53, 0xc0")                        # slot base of rows 128..191's codes: ((0 + 3) & 3) * 64
     a("s_mov_b32 s45, 0")
     a("s_mov_b32 s46, 0")
     a(f"s_movk_i32 s44, {RR}")
     a("s_mov_b32 s52, 0")
     if lds_out:
-        a("v_mov_b32 v90, 0xffffff80")              # producer word at chunk 0: k0 - 128
+        # producer word at chunk 0: rows available (< k0 - 63) - C, one row conservative
+        a(f"v_mov_b32 v90, {(-64 - C) & 0xffffffff:#x}")
         a("v_add_u32 v89, s41, %[lout]")
     if lds_in:
-        a(f"v_mov_b32 v91, {RR + 64}")              # consumer word after chunk 0: 64 consumed (+ R)
+        a(f"v_mov_b32 v91, {RR + C}")               # consumer word after chunk 0: C consumed (+ R)
         a("v_add_u32 v88, s42, %[lin]")
     if gout:
         a("v_mov_b32 v98, %[gooff]")
@@ -353,17 +361,17 @@ def gen_role_ring(IN, OUT_):
         a("v_mov_b32 v101, %[gioff]")
         a("v_mov_b32 v102, %[gipos]")
         a("buffer_load_dwordx2 v[84:85], v101, %[girs], 0 offen sc1")
-    a("ds_read_b128 v[52:55], %[c0]")
-    a("ds_read_b128 v[56:59], %[c0] offset:16")
-    a("ds_read_b128 v[60:63], %[c0] offset:32")
-    a("ds_read_b128 v[64:67], %[c0] offset:48")
+    for q in range(ncr):
+        a(f"ds_read_b128 v[{52 + 4 * q}:{55 + 4 * q}], %[c0]" + (f" offset:{16 * q}" if q else ""))
     a("s_waitcnt vmcnt(0) lgkmcnt(0)")
     a("L_loop_%=:")
     for p in (0, 1):
         cur = 52 if p == 0 else 68
         nxt = 68 if p == 0 else 52
+        refill = p == 0 or C == 64                    # 64 code rows per refill
         lds = []                                      # LDS ops of this chunk top, in issue order
-        # 1. publish the last chunk's outflow
+        # 1. publish the last chunk's outflow (C = 32: lanes 32..63; lanes 0..31 write ahead,
+        # into slots of the next chunk's rows or the ring's slack, never read before rewritten)
         if lds_out:
             if p == 0:
                 a("s_cmp_lt_i32 s44, s40")
@@ -384,54 +392,58 @@ def gen_role_ring(IN, OUT_):
             a("ds_read_b32 v86, %[pin]")
             a("ds_read_b32 v84, v88")
             lds += ["A", "B"]
-        # 3. the raw bytes of chunk c+2 and the granules of chunk c (loaded one chunk ago)
-        stores_after = (2 if gout else 0) + (1 if gin and p == 0 else 0)   # stores issued after those loads
+        # 3. the raw bytes of the refill and the granules of chunk c (loaded one chunk ago); the
+        # stores issued after those loads: the outflow granules (C = 64: mid-chunk and chunk top),
+        # the consumed-rows report (after the last chunk's loads, at p = 1)
+        stores_after = (2 if C == 64 else 1) * gout + (1 if gin and p == 0 else 0)
         a(f"s_waitcnt vmcnt({stores_after})")
         if gin:
-            ring_gin_check(a)
+            ring_gin_check(a, C)
             a(f"s_cbranch_scc1 L_gin{p}_%=")
             a(f"L_ginr{p}_%=:")
             a("v_cndmask_b32_e64 v40, %[ng], v84, s[58:59]")
         elif not lds_in:
             a("v_mov_b32 v40, %[ng]")
-        # 4. codes of chunk c+2 into the wave's code ring (slot base s53, mirror of slots [0, 64))
-        a("v_lshrrev_b32 v94, 1, v93")
-        a("v_lshrrev_b32 v103, 2, v93")
-        a("v_xor_b32 v94, v94, v103")
-        a("v_and_or_b32 v94, v94, 3, 4")
-        a("v_cmp_ne_u32_e64 s[56:57], 0, v93")
-        a("v_cndmask_b32_e64 v94, 0, v94, s[56:57]")
-        a("v_add_u32 v95, s53, %[cwr]")
-        a("ds_write_b8 v95, v94")
-        a("s_cmp_eq_u32 s53, 0")
-        a("s_cselect_b32 s54, 0, 64")                # the mirror (slots 256..319) or the sink (320..383)
-        a("v_add_u32 v95, s54, %[cwm]")
-        a("ds_write_b8 v95, v94")
-        a("s_add_u32 s53, s53, 64")
-        a("s_and_b32 s53, s53, 0xff")
-        lds += ["C1", "C2"]
-        # 5. raw bytes of chunk c+3, granules of chunk c+1
-        a("v_add_u32 v106, 64, v106")
-        a("buffer_load_ubyte v93, v106, %[rrs], 0 offen")
-        if gin:
-            a("v_add_u32 v101, 0x200, v101")
+        # 4. codes of 64 rows (128..191 ahead of the body's first row) into the wave's code
+        # ring (slot base s53, mirror of slots [0, 64))
+        if refill:
+            a("v_lshrrev_b32 v94, 1, v93")
+            a("v_lshrrev_b32 v103, 2, v93")
+            a("v_xor_b32 v94, v94, v103")
+            a("v_and_or_b32 v94, v94, 3, 4")
+            a("v_cmp_ne_u32_e64 s[56:57], 0, v93")
+            a("v_cndmask_b32_e64 v94, 0, v94, s[56:57]")
+            a("v_add_u32 v95, s53, %[cwr]")
+            a("ds_write_b8 v95, v94")
+            a("s_cmp_eq_u32 s53, 0")
+            a("s_cselect_b32 s54, 0, 64")                # the mirror (slots 256..319) or the sink (320..383)
+            a("v_add_u32 v95, s54, %[cwm]")
+            a("ds_write_b8 v95, v94")
+            a("s_add_u32 s53, s53, 64")
+            a("s_and_b32 s53, s53, 0xff")
+            lds += ["C1", "C2"]
+            # 5. raw bytes of the next refill
+            a("v_add_u32 v106, 64, v106")
+            a("buffer_load_ubyte v93, v106, %[rrs], 0 offen")
+        if gin:   # granules of chunk c+1
+            a(f"v_add_u32 v101, {C * 8:#x}, v101")
             a("v_and_b32 v101, %[gimask8], v101")
-            a("v_add_u32 v102, 0x800, v102")
+            a(f"v_add_u32 v102, {C << 5:#x}, v102")
             a("buffer_load_dwordx2 v[84:85], v101, %[girs], 0 offen sc1")
             if p == 1:   # every other chunk: rows consumed (for the producer's back-pressure)
-                a("s_add_u32 s54, s40, 64")
+                a(f"s_add_u32 s54, s40, {C}")
                 a("s_min_i32 s54, s54, %[m]")
                 a("s_add_u32 s54, s54, %[crv0]")
                 a("v_mov_b32 v104, s54")
                 a("buffer_store_dword v104, %[croff], %[cross], 0 offen sc1")
         # 6. row codes of chunk c+1
         a("v_add_u32 v87, %[cbase], v105")
-        for q in range(4):
+        for q in range(ncr):
             a(f"ds_read_b128 v[{nxt + 4 * q}:{nxt + 4 * q + 3}], v87 offset:{16 * q}" if q else
               f"ds_read_b128 v[{nxt}:{nxt + 3}], v87")
-        a("v_add_u32 v105, 64, v105")
+        a(f"v_add_u32 v105, {C}, v105")
         a("v_and_b32 v105, 0xff, v105")
-        lds += ["N1", "N2", "N3", "N4"]
+        lds += ["N%d" % q for q in range(ncr)]
         # 7. LDS inflow: word check, rows into IO, consumed word
         if lds_in:
             after_a = len(lds) - 1 - lds.index("A")
@@ -446,27 +458,27 @@ def gen_role_ring(IN, OUT_):
         else:
             # this chunk's codes (read one chunk ago) must be in: every LDS op since is younger
             a(f"s_waitcnt lgkmcnt({len(lds)})")
-        # 8. 64 steps, 16 groups of 4 rows
-        for u in range(16):
+        # 8. C steps, C/4 groups of 4 rows
+        for u in range(C // 4):
             a(f"v_perm_b32 v48, %[pA], %[k80], v{cur + u}")
             a(f"v_perm_b32 v49, %[pB], %[k80], v{cur + u}")
             for b in range(4):
                 io, l0 = ("v40", "v41") if b % 2 == 0 else ("v41", "v40")
                 step(a, io, l0, b, RING)
-            if gout and u == 7:
+            if gout and C == 64 and u == 7:
                 ring_granule(a)
         # 9. on to the next chunk
-        a("s_add_i32 s40, s40, 64")
+        a(f"s_add_i32 s40, s40, {C}")
         if lds_out:
-            a("s_add_u32 s41, s41, 0x100")
+            a(f"s_add_u32 s41, s41, {4 * C:#x}")
             a(f"s_and_b32 s41, s41, {(RR - 1) * 4:#x}")
             a("v_add_u32 v89, s41, %[lout]")
-            a("v_add_u32 v90, 64, v90")
+            a(f"v_add_u32 v90, {C}, v90")
         if lds_in:
-            a("s_add_u32 s42, s42, 0x100")
+            a(f"s_add_u32 s42, s42, {4 * C:#x}")
             a(f"s_and_b32 s42, s42, {(RR - 1) * 4:#x}")
             a("v_add_u32 v88, s42, %[lin]")
-            a("v_add_u32 v91, 64, v91")
+            a(f"v_add_u32 v91, {C}, v91")
     a("s_cmp_lt_i32 s40, %[end]")
     a("s_cbranch_scc1 L_loop_%=")
     # ---- exit
@@ -505,7 +517,7 @@ def gen_role_ring(IN, OUT_):
             slow_bp_hbm(a, lab, res)
     if gin:
         for p in (0, 1):
-            slow_gin(a, f"L_gin{p}_%=", f"L_ginr{p}_%=")
+            slow_gin(a, f"L_gin{p}_%=", f"L_ginr{p}_%=", C)
     a("L_done_%=:")
     return L
 
@@ -542,7 +554,7 @@ def slow_bp_hbm(a, label, resume):
     a(f"s_branch {resume}")
 
 
-def slow_gin(a, label, resume):
+def slow_gin(a, label, resume, C=64):
     """The chunk's inflow granules are not all published yet: re-load and re-check."""
     a(f"{label}:")
     a("s_add_u32 s46, s46, 1")
@@ -552,7 +564,7 @@ def slow_gin(a, label, resume):
     a("buffer_load_dwordx2 v[84:85], v101, %[girs], 0 offen sc1")
     a("s_memrealtime s[48:49]")
     a("s_waitcnt vmcnt(0) lgkmcnt(0)")
-    ring_gin_check(a)
+    ring_gin_check(a, C)
     a(f"s_cbranch_scc0 {resume}")
     slow_timeout(a, label)
     a(f"{label}_x:")
@@ -567,14 +579,14 @@ CLOBBERS_RING = ['"v%d"' % r for r in range(40, 108) if r != 51] + \
 
 def emit_ring():
     out = ["// GENERATED by tools/gen_flow3.py -- do not edit.  The flow3 ring-mode chunk loops",
-           "// (sw_flow3.hip sw_flow3r_kernel): one inline-asm block per strip role, C = 64, R = %d." % RR,
+           "// (sw_flow3.hip sw_flow3r_kernel): one inline-asm block per (chunk rows C, strip role), R = %d." % RR,
            "// Operands: see F3RLoop in sw_flow3.hip; fixed registers: tools/gen_flow3.py.",
            "#pragma once", ""]
-    for IN in ROLES_IN_RING:
-        for OUT_ in ROLES_OUT:
-            body = gen_role_ring(IN, OUT_)
-            out.append("template <> __device__ __forceinline__ F3Res f3r_loop<F3_%s, F3_%s>(const F3RLoop& x) {"
-                       % (IN.upper(), OUT_.upper()))
+    for C in (64, 32):
+        for IN, OUT_ in [(i, o) for i in ROLES_IN_RING for o in ROLES_OUT]:
+            body = gen_role_ring(IN, OUT_, C)
+            out.append("template <> __device__ __forceinline__ F3Res f3r_loop<%d, F3_%s, F3_%s>(const F3RLoop& x) {"
+                       % (C, IN.upper(), OUT_.upper()))
             out.append("    F3Res r;")
             out.append("    asm volatile(")
             for line in body:

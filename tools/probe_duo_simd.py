@@ -50,6 +50,16 @@ def main():
     t0 = t[:, 2].min()
     beg, end = (t[:, 2] - t0) / 100.0, (t[:, 3] - t0) / 100.0   # us
     print("waves", len(t), "CUs", len(set(key)), "kernel span us %.1f" % (end.max() - beg.min()))
+    print("begin us: min %.1f p25 %.1f median %.1f p75 %.1f max %.1f" % tuple(np.percentile(beg, [0, 25, 50, 75, 100])))
+    print("end us:   min %.1f p25 %.1f median %.1f p75 %.1f max %.1f" % tuple(np.percentile(end, [0, 25, 50, 75, 100])))
+    late = beg > 0.25 * end.max()
+    print("waves beginning after a quarter of the span: %d of %d" % (int(late.sum()), len(t)))
+    # workgroups whose waves overlap in time on one CU
+    by_cu = collections.defaultdict(list)
+    for i in range(0, len(t), 4):
+        by_cu[int(key[i])].append((float(beg[i:i + 4].min()), float(end[i:i + 4].max())))
+    conc = sum(1 for v in by_cu.values() for a in v for b in v if a < b and a[0] < b[1] and b[0] < a[1])
+    print("CUs with 2+ workgroups: %d; overlapping workgroup pairs: %d" % (sum(len(v) > 1 for v in by_cu.values()), conc))
     m = collections.Counter((int(r), int(sm)) for r, sm in zip(role, simd))
     print("role -> SIMD counts:", dict(sorted(m.items())))
     per = collections.defaultdict(list)
