@@ -6,3 +6,4 @@ mkdir -p gpurun_out/lines
 timeout -k 10 240 python bench.py --steps 10 --warmup 2 > gpurun_out/lines/bench_c2.json 2> gpurun_out/lines/bench_c2.err
 timeout -k 10 240 python bench.py --workload batch --steps 5 --warmup 1 > gpurun_out/lines/bench_c3.json 2> gpurun_out/lines/bench_c3.err
 timeout -k 10 240 python bench.py --workload slab --steps 3 --warmup 1 --cpu-seconds 10 > gpurun_out/lines/bench_c5.json 2> gpurun_out/lines/bench_c5.err
+timeout -k 10 240 python bench.py --workload slab --slab-of 8 --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/lines/bench_c5p8.json 2> gpurun_out/lines/bench_c5p8.err
