@@ -84,7 +84,7 @@ def gen_role(IN, OUT_, spec=0, halfpub=True, C=32):
     lds_in, lds_out, gran = IN == "lds", OUT_ == "lds", OUT_ == "gran"
     nd = C // 4                         # row-code dwords per chunk
     ncr = nd // 4                       # their 16-B LDS reads
-    nw = 3 if lds_out else 0            # LDS writes of a chunk's publish
+    nw = 2 if lds_out else 0            # LDS writes of a chunk's publish (ring + mirror in one, the word)
     grows = C // 2 if halfpub else C    # rows per granule publish
     # ---- entry (s_nop 4: the "s" operands may be fresh from v_readfirstlane, and buffer
     # instructions read them as descriptors: 5 wait states)
@@ -127,8 +127,7 @@ def gen_role(IN, OUT_, spec=0, halfpub=True, C=32):
                 a("s_cmp_lt_i32 s44, s40")
                 a(f"s_cbranch_scc1 L_bp{p}_%=")
                 a(f"L_bpr{p}_%=:")
-            a("ds_write_b32 v96, v64")
-            a(f"ds_write_b32 v96, v64 offset:{R * 4}")
+            a(f"ds_write2st64_b32 v96, v64, v64 offset1:{R * 4 // 256}")   # the row and its mirror copy
             a("ds_write_b32 %[pout], v97")
         if gran:
             granule(a, grows)
@@ -171,8 +170,7 @@ def gen_role(IN, OUT_, spec=0, halfpub=True, C=32):
         a("s_cmp_lt_i32 s44, s40")
         a("s_cbranch_scc1 L_bpx_%=")
         a("L_bpxr_%=:")
-        a("ds_write_b32 v96, v64")
-        a(f"ds_write_b32 v96, v64 offset:{R * 4}")
+        a(f"ds_write2st64_b32 v96, v64, v64 offset1:{R * 4 // 256}")
         a(f"v_mov_b32 v97, {BIG:#x}")
         a("ds_write_b32 %[pout], v97")
     if gran:
