@@ -64,7 +64,7 @@ Params g_params;
 
 std::atomic<long long> g_opt_W{0}, g_opt_C{0}, g_opt_bytes{0}, g_opt_timeout{30}, g_opt_blocks{0}, g_opt_orient{0},
     g_opt_mode{-1}, g_opt_trace{0}, g_opt_duo_f16{1}, g_opt_f2stream{0}, g_opt_ring{-1}, g_opt_ring_rows{4096}, g_opt_f2_wgs{0}, g_opt_f2w{0}, g_opt_f2pwg{-1},
-    g_opt_linear{-1}, g_opt_f3{1}, g_opt_slab_plain{0}, g_opt_duo_lds{1}, g_opt_duo_rev{0};
+    g_opt_linear{-1}, g_opt_f3{1}, g_opt_slab_plain{0}, g_opt_duo_lds{1}, g_opt_duo_tab{1};
 
 // Longest sequence the engine takes: granule buffers of m rows keep m * 16 in the
 // 32-bit record count of a buffer resource (sw_device.h linear_edge).
@@ -576,11 +576,11 @@ void profile_words(const Params& p, unsigned out[4]) {
 }
 
 int waves_per_cu(Ctx* c, const LaunchCfg& cfg) {
-    int lw = 0;   // the duo LDS kernel: its dynamic LDS (wrap slots, slot size) bounds the residency
-    while (cfg.duo_wrap > (1 << lw)) ++lw;
-    const int key = (cfg.duo_wrap > 0 ? (lw * 4 + (cfg.f2_lin ? 1 : 0) + (cfg.duo_f16 ? 2 : 0) + 1) * 1000000 : 0) +
-                    cfg.mode * 100000 +
-                    cfg.W * 1000 + cfg.C * 2 + (cfg.dna ? 1 : 0);
+    // the duo LDS kernel: its dynamic LDS (wrap buffer, code table) bounds the residency
+    const int dkb = cfg.duo_wrap > 0 ? (duo_lds_dyn(cfg) + 1023) / 1024 : 0;
+    const int key = (cfg.duo_wrap > 0 ? (dkb * 8 + (cfg.f2_lin ? 1 : 0) + (cfg.duo_f16 ? 2 : 0) + (cfg.duo_tab > 0 ? 4 : 0) + 1) *
+                                            1000000 : 0) +
+                    cfg.mode * 100000 + cfg.W * 1000 + cfg.C * 2 + (cfg.dna ? 1 : 0);
     auto it = c->waves_cache.find(key);
     if (it != c->waves_cache.end()) return it->second;
     int w = cfg.mode == MODE_FLOW2 ? flow2_waves_per_cu(cfg.C) : kernel_waves_per_cu(cfg);
@@ -667,15 +667,21 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
                                     (job.ring && edge == nullptr && (job.C == 64 || job.C == 32)));
     // duo batches at C = 64: strip hand-offs in LDS when the wrap buffer (a round's rows of
     // both pairs) fits the default dynamic-LDS limit; no boundary buffers in HBM then
-    int duo_wrap = 0;
+    // and, at 4 or 8 columns per lane, the row codes from an LDS table when both fit two workgroups per CU
+    int duo_wrap = 0, duo_tab = 0;
     if (duo && job.C == 64 && g_opt_duo_lds.load() != 0) {
         int max_mp = 0;
         for (const DuoDesc& d : job.duos) max_mp = std::max(max_mp, d.m_pad);
         const int slots = duo_wrap_slots(max_mp);
-        if ((long long)slots * (f2_lin ? 4 : 8) <= DUO_LDS_DYN_MAX) {
+        const long long wrap_b = (long long)slots * (f2_lin ? 4 : 8);
+        const int tab_w = DUO_TAB_OFF + max_mp + DUO_TAB_TAIL;
+        if (g_opt_duo_tab.load() != 0 && job.W % 4 == 0 && wrap_b + 4LL * tab_w + 16 <= duo_lds_fit(f2_lin)) {
             duo_wrap = slots;
-            job.bnd_granules = 0;
+            duo_tab = tab_w;
+        } else if (wrap_b <= 64 * 1024) {
+            duo_wrap = slots;
         }
+        if (duo_wrap > 0) job.bnd_granules = 0;
     }
     // read once: it sizes the ring arena here and addresses it in the kernel (kp.ring_rows)
     const long long ring_rows = g_opt_ring_rows.load();
@@ -755,6 +761,7 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
     // option f3 = 0: C2
     cfg.f3 = use_f3;
     cfg.duo_wrap = duo_wrap;
+    cfg.duo_tab = duo_tab;
     if (cfg.f2_w2 && job.C == 16 && !use_f3) {
         set_err("flow2: two columns per lane at C = 16 runs on flow3 only (rows staged in LDS, one GPU)");
         return -1;
@@ -815,10 +822,7 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
         for (int r = 0; r < 4; ++r) w |= (unsigned)(r == q ? 0 : prm.match - prm.mismatch) << (8 * r);
         kp.pen[q] = w;
     }
-    if (duo_wrap > 0) {
-        kp.wrap_rows = duo_wrap;
-        kp.duo_rev = g_opt_duo_rev.load() != 0 ? 1 : 0;
-    }
+    if (duo_wrap > 0) kp.wrap_rows = duo_wrap;
     kp.timeout_ticks = g_opt_timeout.load() * 100000000LL;   // s_memrealtime: 100 MHz
     kp.trace = reinterpret_cast<unsigned long long*>(g_opt_trace.load());
     if (job.ring) {
@@ -847,7 +851,8 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
     t_stats.items = items;
     t_stats.mode = job.mode;
     t_stats.variant = (cfg.duo_f16 ? 1 : 0) | (cfg.f2_stream ? 2 : 0) | (job.ring ? 4 : 0) | (cfg.f2_lin ? 8 : 0) |
-                      (cfg.f2_w2 ? 16 : 0) | (cfg.f2_pwg ? 32 : 0) | (cfg.f3 ? 64 : 0) | (cfg.duo_wrap > 0 ? 128 : 0);
+                      (cfg.f2_w2 ? 16 : 0) | (cfg.f2_pwg ? 32 : 0) | (cfg.f3 ? 64 : 0) | (cfg.duo_wrap > 0 ? 128 : 0) |
+                      (cfg.duo_tab > 0 ? 256 : 0);
     t_stats.boundary_bytes = (long long)(job.bnd_granules * sizeof(Granule));
     c->last = s;
     return 0;
@@ -1620,9 +1625,9 @@ int sw_set_option(const char* key, long long v) {
     } else if (k == "duo_lds") {   // 1 (default): duo strip hand-offs in LDS when the wrap buffer fits, 0: HBM granules
         if (v < 0 || v > 1) return -1;
         g_opt_duo_lds = v;
-    } else if (k == "duo_rev") {   // 1: the duo LDS kernel assigns strip roles by SIMD (complementary per CU)
+    } else if (k == "duo_tab") {   // 1 (default): duo LDS kernel row codes from an LDS table when it fits, 0: carried by DPP
         if (v < 0 || v > 1) return -1;
-        g_opt_duo_rev = v;
+        g_opt_duo_tab = v;
     } else if (k == "slab_plain") {   // 1: exported slab buffers may fall back to plain device memory
         if (v < 0 || v > 1) return -1;
         g_opt_slab_plain = v;
@@ -1661,7 +1666,7 @@ long long sw_get_option(const char* key) {
     if (k == "f3") return g_opt_f3;
     if (k == "slab_plain") return g_opt_slab_plain;
     if (k == "duo_lds") return g_opt_duo_lds;
-    if (k == "duo_rev") return g_opt_duo_rev;
+    if (k == "duo_tab") return g_opt_duo_tab;
     return -1;
 }
 

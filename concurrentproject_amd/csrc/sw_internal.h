@@ -97,7 +97,6 @@ struct KParams {
     int wrap_rows;
     unsigned* ring_cons;          // ring j's consumer progress (positions consumed), RING_CONS_STRIDE apart
     // (the duo kernel with LDS hand-offs takes its wrap-buffer slots from wrap_rows)
-    int duo_rev;                  // duo LDS kernel: strip roles by SIMD (complementary across a CU's workgroups)
 };
 
 constexpr int RING_CONS_STRIDE = 32;   // dwords between consumer progress words (one 128-B line each)
@@ -136,6 +135,7 @@ struct LaunchCfg {
     bool f3 = false;        // MODE_FLOW2 staged two-column linear-gap launch on the flow3 kernel (sw_flow3.hip)
     int duo_wrap = 0;       // MODE_DUO at C = 64: > 0 = strip hand-offs in LDS (sw_duo_lds_kernel), this many
                             // wrap-buffer slots (a power of two >= every m_pad); 0 = HBM granules
+    int duo_tab = 0;        // with duo_wrap, W % 4 == 0: > 0 = row codes from an LDS table of this many words
 };
 // the duo LDS kernel's wrap buffer: slots for rows of m_pad up to m, and its dynamic LDS
 inline int duo_wrap_slots(int m) {
@@ -143,7 +143,17 @@ inline int duo_wrap_slots(int m) {
     while (w < m) w *= 2;
     return w;
 }
-constexpr int DUO_LDS_DYN_MAX = 64 * 1024;   // within the default dynamic-LDS limit, two workgroups per CU
+// the duo LDS kernel's row-code table (sw_kernels.hip StripDuoT): rows -DUO_TAB_OFF .. m_pad + DUO_TAB_TAIL
+constexpr int DUO_TAB_OFF = 528;     // rows below row 0: lane 63's W = 8 positions and a read group ahead
+constexpr int DUO_TAB_TAIL = 768;    // rows past m_pad: the last chunk's steps, the build's two chunks ahead
+// the duo LDS kernel's dynamic LDS: the wrap buffer, then the code table (words, 16-B rounded)
+inline int duo_lds_dyn(const LaunchCfg& cfg) {
+    return cfg.duo_wrap * (cfg.f2_lin ? 4 : 8) + ((cfg.duo_tab * 4 + 15) & ~15);
+}
+constexpr int DUO_LDS_DYN_MAX = 72 * 1024;   // attribute limit of the duo LDS kernel's dynamic LDS
+// the most dynamic LDS that still admits two workgroups per CU beside the static LDS (rings, sinks:
+// ~5 KB at the linear-gap step's 4-B slots, ~9 KB affine)
+inline int duo_lds_fit(bool lin) { return lin ? 72 * 1024 : 68 * 1024; }
 constexpr int F2_WGS_MAX = 4;   // flow2 streamed kernel: most workgroups per CU (launch_c sizes the LDS pad)
 
 // MODE_FLOW stages a pair's row codes in LDS: one byte per row plus the

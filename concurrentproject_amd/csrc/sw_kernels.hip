@@ -857,6 +857,141 @@ struct StripDuo {
     }
 };
 
+// StripDuo with its row codes read from an LDS table (sw_duo_lds_kernel with TAB): the
+// code selector of row r sits at tab[r + DUO_TAB_OFF], so position 0 of lane l takes the
+// code of its row k - W*l at step k from tl[k] (tl = tab + DUO_TAB_OFF - W*l), 4 steps per
+// 16-B read, instead of two DPP moves a step carrying the codes lane to lane.  The code of
+// position p at chunk step K lives in R[(K - p) & 15]: a code enters at position 0 and
+// stays in its register for the W steps it takes to cross the lane; the read for steps
+// K+5..K+8 is issued at step K, into registers whose codes left the lane by step K-1.
+template <int W, bool M3, bool LIN>
+struct StripDuoT {
+    static_assert(W % 4 == 0 && W <= 8, "16-B table reads per 4 steps; a code lives W steps in 16 registers");
+    unsigned pA[W], pB[W];
+    u16x2 aA[W], aB[W];
+    u16x2 hg[W], eh[W], fh[W];
+    unsigned R[16];
+    u16x2 L0, M;
+    unsigned IOA, IOE;
+    const unsigned* tl;
+
+    __device__ __forceinline__ void setup(const KParams& kp, const DuoDesc& d, int strip, int lane, const unsigned* tab) {
+        constexpr int SW = 64 * W;
+        const unsigned char* c0 = kp.seq + d.col_off[0];
+        const unsigned char* c1 = kp.seq + d.col_off[1];
+#pragma unroll
+        for (int p = 0; p < W; ++p) {
+            const int c = strip * SW + lane * W + p;
+            unsigned w0 = 0xFFFFFFFFu, w1 = 0xFFFFFFFFu;
+            if (c < d.n[0]) {
+                const int q = dna_code(c0[c]);
+                w0 = q == 0 ? kp.pen[0] : q == 1 ? kp.pen[1] : q == 2 ? kp.pen[2] : kp.pen[3];
+            }
+            if (c < d.n[1]) {
+                const int q = dna_code(c1[c]);
+                w1 = q == 0 ? kp.pen[0] : q == 1 ? kp.pen[1] : q == 2 ? kp.pen[2] : kp.pen[3];
+            }
+            pA[p] = w0;
+            pB[p] = w1;
+        }
+        const u16x2 ma2 = splat2(kp.match);
+#pragma unroll
+        for (int p = 0; p < W; ++p) {
+            aA[p] = ma2; aB[p] = ma2; hg[p] = splat2(0); eh[p] = splat2(0); fh[p] = splat2(0);
+        }
+        L0 = ma2; M = splat2(0); IOA = as32(ma2); IOE = 0u;
+        tl = tab + DUO_TAB_OFF - W * lane;
+        // codes of steps -8..7 (rows below 0: the table's sentinels)
+#pragma unroll
+        for (int g = -2; g < 2; ++g) load_group(4 * g);
+    }
+
+    __device__ __forceinline__ void load_group(const int k) {   // k: a multiple of 4
+        const u32x4 v = *reinterpret_cast<const u32x4*>(tl + k);
+        const int j = k & 15;
+        R[j] = v.x; R[(j + 1) & 15] = v.y; R[(j + 2) & 15] = v.z; R[(j + 3) & 15] = v.w;
+    }
+
+    // step K (0..15) of a 16-step group starting at strip step kb
+    template <int K>
+    __device__ __forceinline__ void step(u16x2 (&aCur)[W], const u16x2 (&aPrev)[W], const int kb, const u16x2 go2,
+                                         const u16x2 ge2, const u16x2 ma2, const u16x2 gom2) {
+        if constexpr ((K + 5) % 4 == 0) load_group(kb + K + 5);
+        const u16x2 aL0 = as16((unsigned)dpp_shr1((int)IOA, (int)as32(aPrev[W - 1])));
+        u16x2 ehL0 = splat2(0);
+        if constexpr (!LIN) ehL0 = as16((unsigned)dpp_shr1((int)IOE, (int)as32(eh[W - 1])));
+        const u16x2 hgL0 = vsubs2(aL0, gom2);
+        u16x2 tOdd = splat2(0);
+#pragma unroll
+        for (int p = W - 1; p >= 0; --p) {
+            const int q = p > 0 ? p - 1 : 0;
+            const u16x2 hgL = p > 0 ? hg[q] : hgL0;
+            const unsigned rL = R[(K - p + 16) & 15];
+            const u16x2 aD = p > 0 ? aCur[q] : L0;
+            const u16x2 pen = as16(__builtin_amdgcn_perm(pB[p], pA[p], rL));
+            const u16x2 t = vsubs2(aD, pen);
+            u16x2 H;
+            if constexpr (LIN) {
+                H = vmax3h(t, hgL, hg[p]);
+                if (p & 1) tOdd = t;
+                else M = vmax3h(M, tOdd, t);
+            } else {
+                const u16x2 ehL = p > 0 ? eh[q] : ehL0;
+                const u16x2 E = vmax2(ehL, hgL);
+                const u16x2 F = vmax2(fh[p], hg[p]);
+                if constexpr (M3) {
+                    H = vmax3h(t, E, F);
+                    if (p & 1) tOdd = t;
+                    else M = vmax3h(M, tOdd, t);
+                } else {
+                    H = vmax2(vmax2(t, E), F);
+                    M = vmax2(M, t);
+                }
+                eh[p] = vsubs2(E, ge2);
+                fh[p] = vsubs2(F, ge2);
+            }
+            aCur[p] = add2(H, ma2);
+            hg[p] = vsubs2(H, go2);
+        }
+        L0 = aL0;
+        IOA = (unsigned)__builtin_amdgcn_update_dpp((int)as32(aCur[W - 1]), (int)IOA, DPP_WAVE_SHL1, 0xF, 0xF, false);
+        if constexpr (!LIN)
+            IOE = (unsigned)__builtin_amdgcn_update_dpp((int)as32(eh[W - 1]), (int)IOE, DPP_WAVE_SHL1, 0xF, 0xF, false);
+    }
+
+    template <int K>
+    __device__ __forceinline__ void steps(const int kb, const u16x2 go2, const u16x2 ge2, const u16x2 ma2,
+                                          const u16x2 gom2) {
+        if constexpr (K < 16) {
+            if constexpr (K % 2 == 0) step<K>(aA, aB, kb, go2, ge2, ma2, gom2);
+            else step<K>(aB, aA, kb, go2, ge2, ma2, gom2);
+            steps<K + 1>(kb, go2, ge2, ma2, gom2);
+        }
+    }
+
+    // C steps from strip step k0 (a multiple of 16)
+    template <int C>
+    __device__ __forceinline__ void run(const int k0, const u16x2 go2, const u16x2 ge2, const u16x2 ma2,
+                                        const u16x2 gom2) {
+        static_assert(C % 16 == 0, "chunks of whole 16-step groups");
+#pragma unroll
+        for (int s = 0; s < C; s += 16) steps<0>(k0 + s, go2, ge2, ma2, gom2);
+    }
+
+    __device__ __forceinline__ void commit_max(const KParams& kp, const DuoDesc& d, int lane) {
+        int m0 = M.x, m1 = M.y;
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            m0 = max(m0, __shfl_xor(m0, off));
+            m1 = max(m1, __shfl_xor(m1, off));
+        }
+        if (lane == 0) {
+            if (m0 > 0) atomicMax(&kp.scores[d.out_idx[0]], m0);
+            if (m1 > 0 && d.out_idx[1] >= 0) atomicMax(&kp.scores[d.out_idx[1]], m1);
+        }
+    }
+};
+
 __device__ __forceinline__ unsigned codes_duo(unsigned raw0, unsigned raw1, int k0, int lane, int C, const DuoDesc& d) {
     const int row = k0 + lane;
     const bool l0 = lane < C && row >= 0 && row < d.m[0];
@@ -969,32 +1104,63 @@ struct DuoLink {
     const int* cons;     // outflow ring: the consumer's word (positions < *cons are read); null: none
 };
 
-template <int W, int C, bool M3, bool LIN>
+// TAB: the row codes come from the workgroup's LDS table (StripDuoT); `build` (the duo's
+// strip 0, wave 0) writes the table as it goes, two chunks ahead of its own reads and so of
+// every later strip's, after its first 128 rows (and the sentinels below row 0), then sets
+// *ready_out (the other waves wait for it before their first read of this duo's table).
+template <int W, int C, bool M3, bool LIN, bool TAB>
 __device__ void strip_pass_duo_lds(const KParams& kp, const DuoDesc& d, const int strip, const int lane,
                                    const bool has_in, const DuoLink<LIN> in, const bool has_out,
                                    const DuoLink<LIN> out, int* const prod_out, int* const cons_out,
-                                   DuoSlot<LIN>* const sink) {
+                                   DuoSlot<LIN>* const sink, unsigned* const tab, const bool build,
+                                   int* const ready_out, const int ready_val) {
     constexpr int SW = 64 * W;
     static_assert(C == 64, "the LDS links move one row per lane and chunk");
     const int m = d.m_pad;
     const u16x2 go2 = splat2(kp.gap_init), ge2 = splat2(kp.gap_ext), ma2 = splat2(kp.match),
                 gom2 = splat2(kp.gap_init + kp.match);
-    StripDuo<W, M3, LIN> S;
-    S.setup(kp, d, strip, lane);
     const __amdgpu_buffer_rsrc_t r0 =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned char*>(kp.seq + d.row_off[0]), 0, d.m[0], RSRC_FLAGS);
     const __amdgpu_buffer_rsrc_t r1 =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned char*>(kp.seq + d.row_off[1]), 0, d.m[1], RSRC_FLAGS);
     const int nchunks = (m + SW - 1 + C - 1) / C;
+    unsigned raw0_nxt = 0u, raw1_nxt = 0u;
+    if constexpr (TAB) {
+        if (build) {
+            // rows -DUO_TAB_OFF .. 127 now (sentinels below row 0), then 64 rows a chunk
+            for (int i = lane; i < DUO_TAB_OFF + 128; i += 64) {
+                const int row = i - DUO_TAB_OFF;
+                const unsigned q0 = fetch_raw(r0, row, 0, 1, d.m[0]), q1 = fetch_raw(r1, row, 0, 1, d.m[1]);
+                tab[i] = codes_duo(q0, q1, row, 0, 1, d);
+            }
+            raw0_nxt = fetch_raw(r0, 128, lane, C, d.m[0]);
+            raw1_nxt = fetch_raw(r1, 128, lane, C, d.m[1]);
+            compiler_fence();
+            *ready_out = ready_val;   // after the table writes (DS ops execute in order)
+        }
+    } else {
+        raw0_nxt = fetch_raw(r0, 0, lane, C, d.m[0]);
+        raw1_nxt = fetch_raw(r1, 0, lane, C, d.m[1]);
+    }
+    std::conditional_t<TAB, StripDuoT<W, M3, LIN>, StripDuo<W, M3, LIN>> S;
+    if constexpr (TAB) S.setup(kp, d, strip, lane, tab);
+    else S.setup(kp, d, strip, lane);
     const long long t_start = (long long)__builtin_amdgcn_s_memrealtime();
     bool failed = false;
     int cons_seen = 0;
-    unsigned raw0_nxt = fetch_raw(r0, 0, lane, C, d.m[0]), raw1_nxt = fetch_raw(r1, 0, lane, C, d.m[1]);
     for (int c = 0; c < nchunks; ++c) {
         const int k0 = c * C;
         const unsigned raw0 = raw0_nxt, raw1 = raw1_nxt;
-        raw0_nxt = fetch_raw(r0, k0 + C, lane, C, d.m[0]);
-        raw1_nxt = fetch_raw(r1, k0 + C, lane, C, d.m[1]);
+        if constexpr (TAB) {
+            if (build) {   // table rows k0 + 128 .. k0 + 191 (bytes loaded a chunk ago), bytes of the next 64
+                tab[DUO_TAB_OFF + k0 + 128 + lane] = codes_duo(raw0, raw1, k0 + 128, lane, C, d);
+                raw0_nxt = fetch_raw(r0, k0 + 192, lane, C, d.m[0]);
+                raw1_nxt = fetch_raw(r1, k0 + 192, lane, C, d.m[1]);
+            }
+        } else {
+            raw0_nxt = fetch_raw(r0, k0 + C, lane, C, d.m[0]);
+            raw1_nxt = fetch_raw(r1, k0 + C, lane, C, d.m[1]);
+        }
         unsigned va = as32(ma2), ve = 0u;   // no inflow / rows >= m: the border (H = E = 0)
         if (has_in) {
             // the progress word and the chunk's rows in one LDS round trip (a wave's DS ops
@@ -1028,8 +1194,12 @@ __device__ void strip_pass_duo_lds(const KParams& kp, const DuoDesc& d, const in
         }
         S.IOA = va;
         S.IOE = ve;
-        S.IOR = codes_duo(raw0, raw1, k0, lane, C, d);
-        S.template run<C>(go2, ge2, ma2, gom2);
+        if constexpr (TAB) {
+            S.template run<C>(k0, go2, ge2, ma2, gom2);
+        } else {
+            S.IOR = codes_duo(raw0, raw1, k0, lane, C, d);
+            S.template run<C>(go2, ge2, ma2, gom2);
+        }
         if (has_out) {
             // lane L holds the outflow of step k0 + L: row k0 + L - (SW - 1)
             const int row_out = k0 + lane - (SW - 1);
@@ -1063,51 +1233,62 @@ __device__ void strip_pass_duo_lds(const KParams& kp, const DuoDesc& d, const in
     S.commit_max(kp, d, lane);
 }
 
-// kp.wrap_rows: slots of the wrap buffer (a power of two >= every duo's m_pad);
-// kp.duo_rev: strip roles by SIMD (complementary on the two workgroups of a CU), else by wave index
-template <int W, int C, bool M3, bool LIN>
+// kp.wrap_rows: slots of the wrap buffer (a power of two >= every duo's m_pad); TAB: the row-code
+// table follows it in the dynamic LDS (DUO_TAB_OFF + m_pad + DUO_TAB_TAIL words, host-sized).
+// With TAB, one table serves the workgroup's current duo: wave 0 rewrites it for duo i only
+// after every wave has reported done with duo i - 1 (done[]), and the other waves read it
+// only after wave 0 has written its first rows (tabready).  Neither wait closes a cycle:
+// the waves finishing duo i - 1 need nothing from wave 0's duo i.
+template <int W, int C, bool M3, bool LIN, bool TAB>
 __global__ void __launch_bounds__(64 * DUO_WAVES) sw_duo_lds_kernel(KParams kp) {
     static_assert(DUO_WAVES == 4, "the LDS links pair waves w -> w + 1 and 3 -> 0");
     using Slot = DuoSlot<LIN>;
     extern __shared__ __attribute__((aligned(16))) unsigned char duo_dyn[];
     Slot* const wrap = reinterpret_cast<Slot*>(duo_dyn);
+    unsigned* const tab = reinterpret_cast<unsigned*>(duo_dyn + (size_t)kp.wrap_rows * sizeof(Slot));
     __shared__ Slot ring[3][DUO_R];
     __shared__ Slot sink[4][64];
     __shared__ int prod[4], cons[4], psink[4][64];
-    __shared__ int s_simd[4];
+    __shared__ int done[4], tabready;
     const int lane = threadIdx.x & 63;
-    const int hw = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    // the SIMD this wave runs on (HW_REG_HW_ID bits 5:4)
-    const int my_simd = __builtin_amdgcn_readfirstlane((int)((__builtin_amdgcn_s_getreg((31 << 11) | 4) >> 4) & 3));
+    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     if (threadIdx.x < 4) {
         prod[threadIdx.x] = 0;
         cons[threadIdx.x] = 0;
+        done[threadIdx.x] = 0;
     }
-    if (lane == 0) s_simd[hw] = my_simd;
+    if (threadIdx.x == 0) tabready = 0;
     __syncthreads();
-    // strip roles: wave index, or (kp.duo_rev) by SIMD so that the two workgroups sharing a CU
-    // hold complementary roles on each SIMD (r and 3 - r: one starts its strips late where the
-    // other starts early).  The dispatcher places a workgroup's waves on consecutive SIMDs from
-    // the one wave 0 got (observed: 0 for one workgroup of a CU, 1 for the other); roles follow
-    // the SIMD, mirrored when wave 0's SIMD is odd -- only if the 4 SIMDs are distinct, so the
-    // roles are always a permutation of the waves (placement affects speed, never results)
-    int wave = hw;
-    if (kp.duo_rev) {
-        const int s0 = s_simd[0];
-        if (((1 << s0) | (1 << s_simd[1]) | (1 << s_simd[2]) | (1 << s_simd[3])) == 15)
-            wave = (s0 & 1) ? 3 - my_simd : my_simd;
-    }
-    wave = __builtin_amdgcn_readfirstlane(wave);
     const unsigned wmask = (unsigned)kp.wrap_rows - 1u;
     // progress words: lane 0 writes the word, the others a sink (no exec-mask branch)
     int* const prod_out = lane == 0 ? &prod[wave] : &psink[wave][lane];
     int* const cons_out = lane == 0 ? &cons[wave] : &psink[wave][lane];
+    int* const done_out = lane == 0 ? &done[wave] : &psink[wave][lane];
+    int* const ready_out = lane == 0 ? &tabready : &psink[wave][lane];
     int base = 0, prev = 0;   // position bases of this round and the last
+    int dseq = 0;             // duos this workgroup has begun
     // tools/probe_duo_simd.py: where each wave runs (HW_ID: SIMD, CU, SE; XCC_ID) and when
-    const unsigned long long t_begin = kp.trace != nullptr ? __builtin_amdgcn_s_memrealtime() : 0ull;
-    for (int di = blockIdx.x; di < kp.npairs; di += gridDim.x) {
+    const long long t_begin = (long long)__builtin_amdgcn_s_memrealtime();
+    bool failed = false;
+    for (int di = blockIdx.x; di < kp.npairs; di += gridDim.x, ++dseq) {
         const DuoDesc d = load_duo(kp, di);
         const int span = (d.m_pad + 64 * W - 1 + C - 1) / C * C + 128;
+        if constexpr (TAB) {
+            // wave 0: every wave done with the last duo's table; the others: this duo's first rows in
+            if (wave < d.strips && !failed) {
+                for (;;) {
+                    const bool ok = wave == 0 ? min(min(lds_load(&done[1]), lds_load(&done[2])), lds_load(&done[3])) >= dseq
+                                              : lds_load(&tabready) >= dseq + 1;
+                    if (__builtin_amdgcn_readfirstlane((int)ok)) break;
+                    __builtin_amdgcn_s_sleep(1);
+                    if ((long long)__builtin_amdgcn_s_memrealtime() - t_begin > kp.timeout_ticks) {
+                        failed = true;
+                        break;
+                    }
+                }
+                compiler_fence();
+            }
+        }
         for (int r = 0; 4 * r < d.strips; ++r) {
             const int strip = 4 * r + wave;
             if (strip < d.strips) {
@@ -1115,8 +1296,9 @@ __global__ void __launch_bounds__(64 * DUO_WAVES) sw_duo_lds_kernel(KParams kp) 
                                       wave > 0 ? base : 0, wave > 0 ? base : prev, &prod[(wave + 3) & 3], nullptr};
                 const DuoLink<LIN> out{wave < 3 ? ring[wave] : wrap, wave < 3 ? (unsigned)DUO_R - 1u : wmask,
                                        wave < 3 ? base : 0, base, nullptr, wave < 3 ? &cons[wave + 1] : nullptr};
-                strip_pass_duo_lds<W, C, M3, LIN>(kp, d, strip, lane, strip > 0, in, strip + 1 < d.strips, out,
-                                                  prod_out, cons_out, sink[wave]);
+                strip_pass_duo_lds<W, C, M3, LIN, TAB>(kp, d, strip, lane, strip > 0, in, strip + 1 < d.strips, out,
+                                                       prod_out, cons_out, sink[wave], tab, strip == 0, ready_out,
+                                                       dseq + 1);
             }
             // done with every position before the next round, read or not: a producer's back-pressure
             // must not wait on a consumer that skipped rounds (idle waves of a duo's last round) --
@@ -1126,13 +1308,16 @@ __global__ void __launch_bounds__(64 * DUO_WAVES) sw_duo_lds_kernel(KParams kp) 
             prev = base;
             base += span;
         }
+        compiler_fence();
+        *done_out = dseq + 1;   // this wave reads this duo's table no more
     }
+    if (failed && lane == 0) atomicOr(&kp.ctrl->error, ERR_TIMEOUT);
     if (kp.trace != nullptr && lane == 0) {
-        unsigned long long* t = kp.trace + 4ull * (4u * blockIdx.x + (unsigned)hw);
+        unsigned long long* t = kp.trace + 4ull * (4u * blockIdx.x + (unsigned)wave);
         // HW_REG_HW_ID, and the strip role this wave ran at bit 40
         t[0] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4) | ((unsigned long long)wave << 40);
         t[1] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20);   // HW_REG_XCC_ID
-        t[2] = t_begin;
+        t[2] = (unsigned long long)t_begin;
         t[3] = __builtin_amdgcn_s_memrealtime();
     }
 }
@@ -1165,18 +1350,25 @@ hipError_t launch_t(const LaunchCfg& cfg, const KParams& kp, hipStream_t s) {
         case MODE_DUO:
             if constexpr (DNA && C == 64) {
                 if (cfg.duo_wrap > 0) {   // every hand-off in LDS
-                    const int dyn = cfg.duo_wrap * (cfg.f2_lin ? 4 : 8);
+                    const int dyn = duo_lds_dyn(cfg);
                     if (dyn > DUO_LDS_DYN_MAX) return hipErrorInvalidValue;
                     auto go = [&](auto kern) -> hipError_t {
-                        // the wrap buffer and the static rings may pass 64 KB together
+                        // the wrap buffer, the code table and the static rings may pass 64 KB together
                         const hipError_t e = raise_dyn_lds((const void*)kern, DUO_LDS_DYN_MAX);
                         if (e != hipSuccess) return e;
                         hipLaunchKernelGGL(kern, dim3(cfg.blocks), dim3(64 * DUO_WAVES), (size_t)dyn, s, kp);
                         return hipGetLastError();
                     };
-                    if (cfg.duo_f16 && cfg.f2_lin) return go(sw_duo_lds_kernel<W, C, true, true>);
-                    if (cfg.duo_f16) return go(sw_duo_lds_kernel<W, C, true, false>);
-                    return go(sw_duo_lds_kernel<W, C, false, false>);
+                    if constexpr (W % 4 == 0) {
+                        if (cfg.duo_tab > 0) {
+                            if (cfg.duo_f16 && cfg.f2_lin) return go(sw_duo_lds_kernel<W, C, true, true, true>);
+                            if (cfg.duo_f16) return go(sw_duo_lds_kernel<W, C, true, false, true>);
+                            return go(sw_duo_lds_kernel<W, C, false, false, true>);
+                        }
+                    }
+                    if (cfg.duo_f16 && cfg.f2_lin) return go(sw_duo_lds_kernel<W, C, true, true, false>);
+                    if (cfg.duo_f16) return go(sw_duo_lds_kernel<W, C, true, false, false>);
+                    return go(sw_duo_lds_kernel<W, C, false, false, false>);
                 }
             }
             if constexpr (DNA) {
@@ -1200,10 +1392,16 @@ int waves_t(const LaunchCfg& cfg) {
     const int mode = cfg.mode;
     if constexpr (DNA && C == 64) {
         if (mode == MODE_DUO && cfg.duo_wrap > 0) {
-            const int dyn = cfg.duo_wrap * (cfg.f2_lin ? 4 : 8);
-            return cfg.f2_lin    ? occupancy_waves(sw_duo_lds_kernel<W, C, true, true>, 64 * DUO_WAVES, dyn)
-                   : cfg.duo_f16 ? occupancy_waves(sw_duo_lds_kernel<W, C, true, false>, 64 * DUO_WAVES, dyn)
-                                 : occupancy_waves(sw_duo_lds_kernel<W, C, false, false>, 64 * DUO_WAVES, dyn);
+            const int dyn = duo_lds_dyn(cfg);
+            if constexpr (W % 4 == 0) {
+                if (cfg.duo_tab > 0)
+                    return cfg.f2_lin    ? occupancy_waves(sw_duo_lds_kernel<W, C, true, true, true>, 64 * DUO_WAVES, dyn)
+                           : cfg.duo_f16 ? occupancy_waves(sw_duo_lds_kernel<W, C, true, false, true>, 64 * DUO_WAVES, dyn)
+                                         : occupancy_waves(sw_duo_lds_kernel<W, C, false, false, true>, 64 * DUO_WAVES, dyn);
+            }
+            return cfg.f2_lin    ? occupancy_waves(sw_duo_lds_kernel<W, C, true, true, false>, 64 * DUO_WAVES, dyn)
+                   : cfg.duo_f16 ? occupancy_waves(sw_duo_lds_kernel<W, C, true, false, false>, 64 * DUO_WAVES, dyn)
+                                 : occupancy_waves(sw_duo_lds_kernel<W, C, false, false, false>, 64 * DUO_WAVES, dyn);
         }
     }
     switch (mode) {

@@ -194,8 +194,9 @@ void sw_db_close(sw_db* db);
  *              C = 64 (C5); 0 = the compiled flow2 kernel
  *   "duo_lds"  1 = (default) duo batches at C = 64 hand strip edges on in LDS when a round's
  *              rows fit (m <= 16384 linear-gap step, 8192 affine), 0 = through HBM granules
- *   "duo_rev"  1 = the duo LDS kernel assigns strip roles by SIMD, so the two workgroups of a
- *              CU hold complementary roles on each SIMD (pipeline fill), 0 = by wave index
+ *   "duo_tab"  1 = (default) the duo LDS kernel reads its row codes from an LDS table (4 or 8
+ *              columns per lane, when the table and the wrap buffer fit two workgroups per CU),
+ *              0 = the codes travel lane to lane by DPP
  *   "slab_plain" 1 = an exported slab buffer may fall back to plain device memory (one-GPU
  *              tests only; cross-GPU edges need fine-grained memory), 0 = (default) refuse
  *   "trace"    device address of a 16 x u64 per-strip trace buffer, 0 = off (tools)
@@ -215,7 +216,8 @@ typedef struct {
                                bit 2: flow2 ring edges; bit 3: the linear-gap step;
                                bit 4: flow2 two columns per lane; bit 5: flow2 pair per workgroup;
                                bit 6: the flow3 kernel (sw_flow3.hip);
-                               bit 7: duo strip hand-offs in LDS (no boundary buffers) */
+                               bit 7: duo strip hand-offs in LDS (no boundary buffers);
+                               bit 8: duo row codes from an LDS table */
 } sw_stats;
 int sw_last_stats(sw_stats* out);
 

@@ -5,8 +5,9 @@ granule duo kernel (duo_lds = 0) on the same inputs.  Bit-exact integer equality
 Covered: strips per duo 1..7 (rounds with idle waves), rows around the 64-row chunk and
 the 511-step lane skew, ragged pairs padded inside a duo, the linear-gap and the affine
 step (4- and 8-byte slots), grids of 1-3 workgroups (many duos per workgroup, rounds
-crossing duos without a barrier), odd workgroups in reverse wave order (duo_rev), rows
-beyond the LDS wrap buffer (the granule kernel then), and C3 in full against its golden."""
+crossing duos), the row codes from the LDS table (duo_tab = 1, W = 4 / 8) and carried by DPP
+(duo_tab = 0), rows beyond the table's or the wrap buffer's LDS (the next kernel down then), and
+C3 in full against its golden."""
 import numpy as np
 import pytest
 
@@ -34,11 +35,11 @@ def _defaults(engine):
         engine.set_option(k, 0)
     engine.set_option("mode", -1)
     engine.set_option("duo_lds", 1)
-    engine.set_option("duo_rev", 0)
+    engine.set_option("duo_tab", 1)
     engine.set_option("linear", -1)
 
 
-def _check(engine, oracle_mod, pairs, prm, lds_expected=True, W=8):
+def _check(engine, oracle_mod, pairs, prm, lds_expected=True, W=8, tab_expected=None):
     """The duo kernel at W columns per lane and 64-row chunks (the LDS links' chunk)."""
     op = oracle_mod.Params(prm.match, prm.mismatch, prm.gap_init, prm.gap_ext)
     exp = [oracle_mod.score_linear(a, b, op) for a, b in pairs]
@@ -52,6 +53,8 @@ def _check(engine, oracle_mod, pairs, prm, lds_expected=True, W=8):
     assert bool(st["variant"] & 128) == lds_expected, st
     if lds_expected:
         assert st["boundary_bytes"] == 0, st
+    if tab_expected is not None:
+        assert bool(st["variant"] & 256) == tab_expected, st
     assert got == exp, ("lds", prm)
     engine.set_option("duo_lds", 0)
     assert engine.score_batch(pairs, prm) == exp, ("granules", prm)
@@ -78,46 +81,53 @@ def test_duo_lds_strip_counts_and_rows(engine, oracle_mod, prm_t):
     for lin in ((-1, 0) if prm.gap_init == prm.gap_ext else (-1,)):
         engine.set_option("linear", lin)
         for W in (8, 4):
-            _check(engine, oracle_mod, pairs, prm, W=W)
+            for tab in (1, 0):
+                engine.set_option("duo_tab", tab)
+                _check(engine, oracle_mod, pairs, prm, W=W, tab_expected=bool(tab))
+        engine.set_option("duo_tab", 1)
 
 
-def test_duo_lds_grids_and_reverse_roles(engine, oracle_mod):
-    """11 duos on grids of 1, 2 and 3 workgroups (a workgroup's waves run from one duo into
-    the next with no barrier, positions continuing across rounds and duos), with the strip
-    roles in reverse wave order on odd workgroups and without."""
+def test_duo_lds_grids_many_duos(engine, oracle_mod):
+    """11 duos on grids of 1, 2 and 3 workgroups: a workgroup's waves run from one duo into the
+    next (positions continuing across rounds and duos; with the code table, wave 0 rewrites it
+    for the next duo once every wave is done with the last), table and DPP codes."""
     rng = np.random.default_rng(9)
     pairs = [_related(rng, int(rng.integers(300, 4200)), int(rng.integers(50, 3000))) for _ in range(22)]
     for prm in (engine.Params(), engine.Params(2, -3, 5, 2)):
-        for rev in (0, 1):
-            engine.set_option("duo_rev", rev)
+        for tab in (1, 0):
+            engine.set_option("duo_tab", tab)
             for blocks in (1, 2, 3):
                 engine.set_option("blocks", blocks)
-                _check(engine, oracle_mod, pairs, prm)
+                _check(engine, oracle_mod, pairs, prm, tab_expected=bool(tab))
     engine.set_option("blocks", 0)
+    engine.set_option("duo_tab", 1)
 
 
 def test_duo_lds_wrap_buffer_limit(engine, oracle_mod):
-    """The wrap buffer holds a round's rows in at most 64 KB of LDS: m_pad <= 16384 at the
-    linear-gap step (4-byte slots), <= 8192 affine (8 bytes); longer rows take the granule
-    kernel, with the same scores."""
+    """The LDS kernel's dynamic LDS admits two workgroups per CU: with the code table up to
+    m_pad = 8192 at the linear-gap step (4-B slots: 32 KB wrap buffer + 38 KB table) and 4096
+    affine; without the table the wrap buffer alone up to 16384 / 8192; longer rows take the
+    granule kernel.  Same scores everywhere."""
     rng = np.random.default_rng(4)
-    for prm, m_ok, m_over in ((1, 16384, 16385), (0, 8192, 8193)):
-        p = engine.Params() if prm else engine.Params(2, -3, 5, 2)
-        for m, lds in ((m_ok, True), (m_over, False)):
+    for lin, cases in ((True, ((8192, True, True), (8193, True, False), (16384, True, False), (16385, False, False))),
+                       (False, ((4096, True, True), (4097, True, False), (8192, True, False), (8193, False, False)))):
+        p = engine.Params() if lin else engine.Params(2, -3, 5, 2)
+        for m, lds, tab in cases:
             pairs = [_related(rng, 700, m), _related(rng, 1300, m - 7), (_rand_dna(rng, 90), _rand_dna(rng, 40))]
-            _check(engine, oracle_mod, pairs, p, lds_expected=lds)
+            _check(engine, oracle_mod, pairs, p, lds_expected=lds, tab_expected=tab if lds else None)
 
 
 def test_duo_lds_c3_golden(engine, golden):
-    """C3 (1024 pairs N = 8192, the reference-pinned golden) on the LDS duo kernel, in both
-    wave orders; no strip-boundary buffer in HBM."""
+    """C3 (1024 pairs N = 8192, the reference-pinned golden) on the LDS duo kernel, row codes
+    from the LDS table and by DPP; no strip-boundary buffer in HBM."""
     c = golden("configs.json")["C3"]
     N = c["N"]
     arena = engine.gen_batch(c["seed_base"], c["npairs"], N)
     pairs = [(arena[2 * N * k:2 * N * k + N], arena[2 * N * k + N:2 * N * (k + 1)]) for k in range(c["npairs"])]
-    for rev in (0, 1):
-        engine.set_option("duo_rev", rev)
+    for tab in (1, 0):
+        engine.set_option("duo_tab", tab)
         got = engine.score_batch(pairs)
         st = engine.last_stats()
         assert st["mode"] == 3 and st["variant"] & 128 and st["boundary_bytes"] == 0, st
-        assert got == c["scores"], rev
+        assert bool(st["variant"] & 256) == bool(tab), st
+        assert got == c["scores"], tab

@@ -4,7 +4,7 @@ option; per wave HW_ID (SIMD, CU, SH, SE), XCC_ID, begin and end (s_memrealtime,
 Prints how strip roles map to SIMDs on the CUs that hold two workgroups, and the per-SIMD
 idle time at the start and end of the launch.
 
-    python tools/probe_duo_simd.py [duo_rev]
+    python tools/probe_duo_simd.py [duo_tab]
 """
 import collections
 import os
@@ -25,7 +25,7 @@ def main():
     scores = torch.zeros(P, dtype=torch.int32, device="cuda")
     offs_a = [2 * N * k for k in range(P)]
     offs_b = [2 * N * k + N for k in range(P)]
-    sw.set_option("duo_rev", rev)
+    sw.set_option("duo_tab", rev)
     s = torch.cuda.current_stream()
     trace = None
     for it in range(3):
