@@ -64,7 +64,7 @@ Params g_params;
 
 std::atomic<long long> g_opt_W{0}, g_opt_C{0}, g_opt_bytes{0}, g_opt_timeout{30}, g_opt_blocks{0}, g_opt_orient{0},
     g_opt_mode{-1}, g_opt_trace{0}, g_opt_duo_f16{1}, g_opt_f2stream{0}, g_opt_ring{-1}, g_opt_ring_rows{4096}, g_opt_f2_wgs{0}, g_opt_f2w{0}, g_opt_f2pwg{-1},
-    g_opt_linear{-1}, g_opt_f3{1}, g_opt_slab_plain{0}, g_opt_duo_lds{1}, g_opt_duo_tab{1};
+    g_opt_linear{-1}, g_opt_f3{1}, g_opt_slab_plain{0}, g_opt_duo_lds{1}, g_opt_duo_tab{1}, g_opt_duo_roles{1};
 
 // Longest sequence the engine takes: granule buffers of m rows keep m * 16 in the
 // 32-bit record count of a buffer resource (sw_device.h linear_edge).
@@ -668,6 +668,8 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
     // duo batches at C = 64: strip hand-offs in LDS when the wrap buffer (a round's rows of
     // both pairs) fits the default dynamic-LDS limit; no boundary buffers in HBM then
     // and, at 4 or 8 columns per lane, the row codes from an LDS table when both fit two workgroups per CU
+    // and the duos run in one pass at that (C3, 512 duos: 6.80 -> 6.54 ms); more duos keep the table-less
+    // kernel, whose smaller LDS admits 4 per CU (8192 pairs of 8192: 51.3 ms against 52.0 with the table)
     int duo_wrap = 0, duo_tab = 0;
     if (duo && job.C == 64 && g_opt_duo_lds.load() != 0) {
         int max_mp = 0;
@@ -675,7 +677,8 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
         const int slots = duo_wrap_slots(max_mp);
         const long long wrap_b = (long long)slots * (f2_lin ? 4 : 8);
         const int tab_w = DUO_TAB_OFF + max_mp + DUO_TAB_TAIL;
-        if (g_opt_duo_tab.load() != 0 && job.W % 4 == 0 && wrap_b + 4LL * tab_w + 16 <= duo_lds_fit(f2_lin)) {
+        const bool one_pass = (long long)job.duos.size() <= 2LL * c->cus || g_opt_duo_tab.load() == 2;
+        if (g_opt_duo_tab.load() != 0 && one_pass && job.W % 4 == 0 && wrap_b + 4LL * tab_w + 16 <= duo_lds_fit(f2_lin)) {
             duo_wrap = slots;
             duo_tab = tab_w;
         } else if (wrap_b <= 64 * 1024) {
@@ -728,6 +731,10 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
         job.bnd_granules = (uint64_t)(ring_blocks - 1) * (uint64_t)ring_rows + (uint64_t)wrap_rows;
         if (c->cons.ensure((size_t)ring_blocks * RING_CONS_STRIDE, s)) return -1;
         HIPCHK(hipMemsetAsync(c->cons.p, 0, (size_t)ring_blocks * RING_CONS_STRIDE * sizeof(unsigned), s));
+    }
+    if (duo_wrap > 0 && g_opt_duo_roles.load() != 0) {   // one word per CU (XCC, SE, SH, CU of HW_ID)
+        if (c->cons.ensure(DUO_CU_WORDS, s)) return -1;
+        HIPCHK(hipMemsetAsync(c->cons.p, 0, DUO_CU_WORDS * sizeof(unsigned), s));
     }
     if (job.bnd_granules) {
         size_t freeb = 0, totb = 0;
@@ -822,7 +829,10 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
         for (int r = 0; r < 4; ++r) w |= (unsigned)(r == q ? 0 : prm.match - prm.mismatch) << (8 * r);
         kp.pen[q] = w;
     }
-    if (duo_wrap > 0) kp.wrap_rows = duo_wrap;
+    if (duo_wrap > 0) {
+        kp.wrap_rows = duo_wrap;
+        if (g_opt_duo_roles.load() != 0) kp.ring_cons = c->cons.p;   // per-CU role words (zeroed above)
+    }
     kp.timeout_ticks = g_opt_timeout.load() * 100000000LL;   // s_memrealtime: 100 MHz
     kp.trace = reinterpret_cast<unsigned long long*>(g_opt_trace.load());
     if (job.ring) {
@@ -1625,8 +1635,12 @@ int sw_set_option(const char* key, long long v) {
     } else if (k == "duo_lds") {   // 1 (default): duo strip hand-offs in LDS when the wrap buffer fits, 0: HBM granules
         if (v < 0 || v > 1) return -1;
         g_opt_duo_lds = v;
-    } else if (k == "duo_tab") {   // 1 (default): duo LDS kernel row codes from an LDS table when it fits, 0: carried by DPP
+    } else if (k == "duo_roles") {   // 1 (default): duo strip roles complementary per SIMD across a CU's workgroups
         if (v < 0 || v > 1) return -1;
+        g_opt_duo_roles = v;
+    } else if (k == "duo_tab") {   // 1 (default): duo LDS kernel row codes from an LDS table for one-pass batches,
+        // 2: whenever it fits, 0: carried by DPP
+        if (v < 0 || v > 2) return -1;
         g_opt_duo_tab = v;
     } else if (k == "slab_plain") {   // 1: exported slab buffers may fall back to plain device memory
         if (v < 0 || v > 1) return -1;
@@ -1667,6 +1681,7 @@ long long sw_get_option(const char* key) {
     if (k == "slab_plain") return g_opt_slab_plain;
     if (k == "duo_lds") return g_opt_duo_lds;
     if (k == "duo_tab") return g_opt_duo_tab;
+    if (k == "duo_roles") return g_opt_duo_roles;
     return -1;
 }
 

@@ -95,7 +95,8 @@ struct KParams {
     // j = G-1), so the boundary state is O(G*ring_rows + m), not O(groups*m).
     int ring_rows;
     int wrap_rows;
-    unsigned* ring_cons;          // ring j's consumer progress (positions consumed), RING_CONS_STRIDE apart
+    unsigned* ring_cons;          // ring j's consumer progress (positions consumed), RING_CONS_STRIDE apart;
+                                  // duo LDS kernel: DUO_CU_WORDS zeroed role words (or null)
     // (the duo kernel with LDS hand-offs takes its wrap-buffer slots from wrap_rows)
 };
 
@@ -151,6 +152,7 @@ inline int duo_lds_dyn(const LaunchCfg& cfg) {
     return cfg.duo_wrap * (cfg.f2_lin ? 4 : 8) + ((cfg.duo_tab * 4 + 15) & ~15);
 }
 constexpr int DUO_LDS_DYN_MAX = 72 * 1024;   // attribute limit of the duo LDS kernel's dynamic LDS
+constexpr int DUO_CU_WORDS = 8 * 256;         // duo strip roles: a word per (XCC, SE, SH, CU) of HW_ID
 // the most dynamic LDS that still admits two workgroups per CU beside the static LDS (rings, sinks:
 // ~5 KB at the linear-gap step's 4-B slots, ~9 KB affine)
 inline int duo_lds_fit(bool lin) { return lin ? 72 * 1024 : 68 * 1024; }

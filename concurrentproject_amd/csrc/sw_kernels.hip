@@ -1233,7 +1233,8 @@ __device__ void strip_pass_duo_lds(const KParams& kp, const DuoDesc& d, const in
     S.commit_max(kp, d, lane);
 }
 
-// kp.wrap_rows: slots of the wrap buffer (a power of two >= every duo's m_pad); TAB: the row-code
+// kp.wrap_rows: slots of the wrap buffer (a power of two >= every duo's m_pad); kp.ring_cons: per-CU
+// words for the strip-role assignment (below), or null (roles by wave index); TAB: the row-code
 // table follows it in the dynamic LDS (DUO_TAB_OFF + m_pad + DUO_TAB_TAIL words, host-sized).
 // With TAB, one table serves the workgroup's current duo: wave 0 rewrites it for duo i only
 // after every wave has reported done with duo i - 1 (done[]), and the other waves read it
@@ -1250,15 +1251,48 @@ __global__ void __launch_bounds__(64 * DUO_WAVES) sw_duo_lds_kernel(KParams kp) 
     __shared__ Slot sink[4][64];
     __shared__ int prod[4], cons[4], psink[4][64];
     __shared__ int done[4], tabready;
+    __shared__ int s_simd[4], s_roles;
     const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int hw = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const unsigned hwid = __builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_REG_HW_ID: SIMD 5:4, CU 11:8, SH 12, SE 15:13
+    const int my_simd = __builtin_amdgcn_readfirstlane((int)((hwid >> 4) & 3));
     if (threadIdx.x < 4) {
         prod[threadIdx.x] = 0;
         cons[threadIdx.x] = 0;
         done[threadIdx.x] = 0;
     }
     if (threadIdx.x == 0) tabready = 0;
+    if (lane == 0) s_simd[hw] = my_simd;
     __syncthreads();
+    // Strip roles (kp.ring_cons: one zeroed word per CU).  Two duo workgroups share a CU and its
+    // 4 SIMDs; the older one gets most issue slots, and a role-r wave idles (r x 576 steps) until
+    // the pipeline reaches it.  The second workgroup on a CU takes, on each SIMD, the role 3 - r
+    // of the first one's wave there, so one wave of each SIMD starts early and one late.  Roles
+    // follow the SIMDs only when this workgroup's 4 waves sit on 4 distinct SIMDs, so they are a
+    // permutation of the waves whatever the placement (placement affects speed, never results).
+    int wave = hw;
+    if (kp.ring_cons != nullptr) {
+        if (threadIdx.x == 0) {
+            const int s0 = s_simd[0];
+            int roles = -1;
+            if (((1 << s0) | (1 << s_simd[1]) | (1 << s_simd[2]) | (1 << s_simd[3])) == 15) {
+                const unsigned xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20) & 7u;   // HW_REG_XCC_ID
+                const unsigned key = (xcc << 8) | (((hwid >> 13) & 7u) << 5) | (((hwid >> 12) & 1u) << 4) | ((hwid >> 8) & 15u);
+                const unsigned old = atomicCAS(kp.ring_cons + key, 0u, (1u << 16) | (unsigned)s0);
+                if (old == 0u) roles = 0;                                   // first on this CU: its own order
+                else if ((old >> 16) == 1u) {                               // second: mirror the first
+                    atomicAdd(kp.ring_cons + key, 1u << 16);
+                    roles = 16 | (int)(old & 3u);
+                }
+            }
+            s_roles = roles;
+        }
+        __syncthreads();
+        const int roles = s_roles;
+        if (roles == 0) wave = (my_simd - s_simd[0]) & 3;
+        else if (roles > 0) wave = 3 - ((my_simd - (roles & 3)) & 3);
+    }
+    wave = __builtin_amdgcn_readfirstlane(wave);
     const unsigned wmask = (unsigned)kp.wrap_rows - 1u;
     // progress words: lane 0 writes the word, the others a sink (no exec-mask branch)
     int* const prod_out = lane == 0 ? &prod[wave] : &psink[wave][lane];

@@ -194,9 +194,12 @@ void sw_db_close(sw_db* db);
  *              C = 64 (C5); 0 = the compiled flow2 kernel
  *   "duo_lds"  1 = (default) duo batches at C = 64 hand strip edges on in LDS when a round's
  *              rows fit (m <= 16384 linear-gap step, 8192 affine), 0 = through HBM granules
+ *   "duo_roles" 1 = (default) the two duo LDS workgroups of a CU take complementary strip roles
+ *              on each SIMD (one wave starts early, one late), 0 = roles by wave index
  *   "duo_tab"  1 = (default) the duo LDS kernel reads its row codes from an LDS table (4 or 8
- *              columns per lane, when the table and the wrap buffer fit two workgroups per CU),
- *              0 = the codes travel lane to lane by DPP
+ *              columns per lane, when the table and the wrap buffer fit two workgroups per CU
+ *              and the duos run in one pass at that), 2 = whenever it fits, 0 = the codes travel
+ *              lane to lane by DPP
  *   "slab_plain" 1 = an exported slab buffer may fall back to plain device memory (one-GPU
  *              tests only; cross-GPU edges need fine-grained memory), 0 = (default) refuse
  *   "trace"    device address of a 16 x u64 per-strip trace buffer, 0 = off (tools)

@@ -119,15 +119,20 @@ def test_duo_lds_wrap_buffer_limit(engine, oracle_mod):
 
 def test_duo_lds_c3_golden(engine, golden):
     """C3 (1024 pairs N = 8192, the reference-pinned golden) on the LDS duo kernel, row codes
-    from the LDS table and by DPP; no strip-boundary buffer in HBM."""
+    from the LDS table and by DPP, strip roles per CU and by wave index; no strip-boundary
+    buffer in HBM."""
     c = golden("configs.json")["C3"]
     N = c["N"]
     arena = engine.gen_batch(c["seed_base"], c["npairs"], N)
     pairs = [(arena[2 * N * k:2 * N * k + N], arena[2 * N * k + N:2 * N * (k + 1)]) for k in range(c["npairs"])]
-    for tab in (1, 0):
-        engine.set_option("duo_tab", tab)
-        got = engine.score_batch(pairs)
-        st = engine.last_stats()
-        assert st["mode"] == 3 and st["variant"] & 128 and st["boundary_bytes"] == 0, st
-        assert bool(st["variant"] & 256) == bool(tab), st
-        assert got == c["scores"], tab
+    try:
+        for tab, roles in ((1, 1), (1, 0), (0, 1)):
+            engine.set_option("duo_tab", tab)
+            engine.set_option("duo_roles", roles)
+            got = engine.score_batch(pairs)
+            st = engine.last_stats()
+            assert st["mode"] == 3 and st["variant"] & 128 and st["boundary_bytes"] == 0, st
+            assert bool(st["variant"] & 256) == bool(tab), st
+            assert got == c["scores"], (tab, roles)
+    finally:
+        engine.set_option("duo_roles", 1)
