@@ -804,10 +804,11 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
     kp.scores = d_scores;
     kp.npairs = (int)np;
     kp.total_items = items;
-    // epochs are never 0 (tag of a zeroed granule), nor the one that makes flow3's granule
-    // key epoch ^ 0x5BD1E995 zero (a zeroed 8-B granule would then pass its check)
+    // epochs are never 0 (tag of a zeroed granule), nor one that makes flow3's granule key
+    // k = epoch ^ 0x5BD1E995 zero in its low 5 bits: a zeroed 8-B granule passes its check when
+    // its second word equals k (staged) or k ^ (position << 5) (ring edges), which needs exactly that
     do ++c->epoch;
-    while (c->epoch == 0 || c->epoch == 0x5BD1E995u);
+    while (c->epoch == 0 || ((c->epoch ^ 0x5BD1E995u) & 31u) == 0);
     kp.epoch = c->epoch;
     kp.match = prm.match;
     kp.mismatch = prm.mismatch;
