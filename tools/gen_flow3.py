@@ -284,7 +284,6 @@ def emit(spec=0, halfpub=True):
 # the position term rejects a slot still holding an earlier round's row (same epoch).
 # ============================================================================================
 RR = 512                 # LDS ring rows per in-workgroup link (sw_flow3.hip F3R_R)
-CR = 4096                # shared code ring slots (sw_flow3.hip F3R_CR): > the 4 waves' spread (3 links of RR)
 RING = dict(H="v42", HGO="v43", HB="v44", HGOB="v45", TA="v46", TB="v47", PA="v48", PB="v49", M="v50")
 
 
@@ -367,9 +366,7 @@ def gen_role_ring(IN, OUT_, C=64):
     for p in (0, 1):
         cur = 52 if p == 0 else 68
         nxt = 68 if p == 0 else 52
-        # 64 code rows per refill, into the workgroup's shared code ring: by the wave without an LDS
-        # inflow (the group's first strip), whose reads lead every other wave's
-        refill = (p == 0 or C == 64) and not lds_in
+        refill = p == 0 or C == 64                    # 64 code rows per refill
         lds = []                                      # LDS ops of this chunk top, in issue order
         # 1. publish the last chunk's outflow (C = 32: lanes 32..63; lanes 0..31 write ahead,
         # into slots of the next chunk's rows or the ring's slack, never read before rewritten)
@@ -405,7 +402,7 @@ def gen_role_ring(IN, OUT_, C=64):
             a("v_cndmask_b32_e64 v40, %[ng], v84, s[58:59]")
         elif not lds_in:
             a("v_mov_b32 v40, %[ng]")
-        # 4. codes of 64 rows (128..191 ahead of the body's first row) into the shared code
+        # 4. codes of 64 rows (128..191 ahead of the body's first row) into the wave's code
         # ring (slot base s53, mirror of slots [0, 64))
         if refill:
             a("v_lshrrev_b32 v94, 1, v93")
@@ -417,11 +414,11 @@ def gen_role_ring(IN, OUT_, C=64):
             a("v_add_u32 v95, s53, %[cwr]")
             a("ds_write_b8 v95, v94")
             a("s_cmp_eq_u32 s53, 0")
-            a("s_cselect_b32 s54, 0, 64")                # the mirror (slots CR..CR+63) or the sink (CR+64..)
+            a("s_cselect_b32 s54, 0, 64")                # the mirror (slots 256..319) or the sink (320..383)
             a("v_add_u32 v95, s54, %[cwm]")
             a("ds_write_b8 v95, v94")
             a("s_add_u32 s53, s53, 64")
-            a(f"s_and_b32 s53, s53, {CR - 1:#x}")
+            a("s_and_b32 s53, s53, 0xff")
             lds += ["C1", "C2"]
             # 5. raw bytes of the next refill
             a("v_add_u32 v106, 64, v106")
@@ -443,7 +440,7 @@ def gen_role_ring(IN, OUT_, C=64):
             a(f"ds_read_b128 v[{nxt + 4 * q}:{nxt + 4 * q + 3}], v87 offset:{16 * q}" if q else
               f"ds_read_b128 v[{nxt}:{nxt + 3}], v87")
         a(f"v_add_u32 v105, {C}, v105")
-        a(f"v_and_b32 v105, {CR - 1:#x}, v105")
+        a("v_and_b32 v105, 0xff, v105")
         lds += ["N%d" % q for q in range(ncr)]
         # 7. LDS inflow: word check, rows into IO, consumed word
         if lds_in:
