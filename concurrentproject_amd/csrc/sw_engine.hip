@@ -64,7 +64,7 @@ Params g_params;
 
 std::atomic<long long> g_opt_W{0}, g_opt_C{0}, g_opt_bytes{0}, g_opt_timeout{30}, g_opt_blocks{0}, g_opt_orient{0},
     g_opt_mode{-1}, g_opt_trace{0}, g_opt_duo_f16{1}, g_opt_f2stream{0}, g_opt_ring{-1}, g_opt_ring_rows{4096}, g_opt_f2_wgs{0}, g_opt_f2w{0}, g_opt_f2pwg{-1},
-    g_opt_linear{-1}, g_opt_f3{1}, g_opt_slab_plain{0}, g_opt_duo_lds{1}, g_opt_duo_tab{1}, g_opt_duo_roles{1};
+    g_opt_linear{-1}, g_opt_f3{1}, g_opt_slab_plain{0}, g_opt_duo_lds{1}, g_opt_duo_tab{1}, g_opt_duo_roles{1}, g_opt_f3hl{0};
 
 // Longest sequence the engine takes: granule buffers of m rows keep m * 16 in the
 // 32-bit record count of a buffer resource (sw_device.h linear_edge).
@@ -454,8 +454,9 @@ int finalize_mode(Job& job, const Params& prm, int cus) {
             if (job.ring && g_opt_C.load() == 0) job.C = 64;
             // the staged two-column kernel on flow3 (C2): 16-row chunks, whose shorter hand-off lag
             // (63 + 16 steps a strip) outweighs their per-chunk work there (2.70 -> 2.65 ms)
+            // (option f3hl: 32-row chunks whose in-workgroup links hand off every half chunk instead)
             if (!job.ring && !job.f2_stream && !job.slab && job.f2w2 && g_opt_C.load() == 0 && g_opt_f3.load() != 0 &&
-                flow3_fits(max_m, 16))
+                g_opt_f3hl.load() == 0 && flow3_fits(max_m, 16))
                 job.C = 16;
             return 0;
         }
@@ -767,6 +768,7 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
     // the staged two-column linear-gap kernel with hand-scheduled chunk loops (sw_flow3.hip), unless
     // option f3 = 0: C2
     cfg.f3 = use_f3;
+    cfg.f3_hl = use_f3 && !job.ring && job.C == 32 && g_opt_f3hl.load() != 0;
     cfg.duo_wrap = duo_wrap;
     cfg.duo_tab = duo_tab;
     if (cfg.f2_w2 && job.C == 16 && !use_f3) {
@@ -863,7 +865,7 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
     t_stats.mode = job.mode;
     t_stats.variant = (cfg.duo_f16 ? 1 : 0) | (cfg.f2_stream ? 2 : 0) | (job.ring ? 4 : 0) | (cfg.f2_lin ? 8 : 0) |
                       (cfg.f2_w2 ? 16 : 0) | (cfg.f2_pwg ? 32 : 0) | (cfg.f3 ? 64 : 0) | (cfg.duo_wrap > 0 ? 128 : 0) |
-                      (cfg.duo_tab > 0 ? 256 : 0);
+                      (cfg.duo_tab > 0 ? 256 : 0) | (cfg.f3_hl ? 512 : 0);
     t_stats.boundary_bytes = (long long)(job.bnd_granules * sizeof(Granule));
     c->last = s;
     return 0;
@@ -1636,6 +1638,9 @@ int sw_set_option(const char* key, long long v) {
     } else if (k == "duo_lds") {   // 1 (default): duo strip hand-offs in LDS when the wrap buffer fits, 0: HBM granules
         if (v < 0 || v > 1) return -1;
         g_opt_duo_lds = v;
+    } else if (k == "f3hl") {   // 1: flow3 staged launches at C = 32 with half-chunk in-workgroup links (auto C: 32)
+        if (v < 0 || v > 1) return -1;
+        g_opt_f3hl = v;
     } else if (k == "duo_roles") {   // 1 (default): duo strip roles complementary per SIMD across a CU's workgroups
         if (v < 0 || v > 1) return -1;
         g_opt_duo_roles = v;
@@ -1683,6 +1688,7 @@ long long sw_get_option(const char* key) {
     if (k == "duo_lds") return g_opt_duo_lds;
     if (k == "duo_tab") return g_opt_duo_tab;
     if (k == "duo_roles") return g_opt_duo_roles;
+    if (k == "f3hl") return g_opt_f3hl;
     return -1;
 }
 

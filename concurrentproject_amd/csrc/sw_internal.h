@@ -134,6 +134,7 @@ struct LaunchCfg {
     bool f2_w2 = false;     // MODE_FLOW2 with f2_lin: two columns per lane (126 new columns per strip)
     bool f2_pwg = false;    // MODE_FLOW2 batch: a pair per workgroup, all hand-offs in LDS (C = 64, streamed)
     bool f3 = false;        // MODE_FLOW2 staged two-column linear-gap launch on the flow3 kernel (sw_flow3.hip)
+    bool f3_hl = false;     // flow3 staged at C = 32: in-workgroup links hand off every half chunk
     int duo_wrap = 0;       // MODE_DUO at C = 64: > 0 = strip hand-offs in LDS (sw_duo_lds_kernel), this many
                             // wrap-buffer slots (a power of two >= every m_pad); 0 = HBM granules
     int duo_tab = 0;        // with duo_wrap, W % 4 == 0: > 0 = row codes from an LDS table of this many words

@@ -57,8 +57,9 @@ def test_flow3_ragged(engine, oracle_mod):
     engine.set_option("orient", 1)
     engine.set_option("mode", 5)      # flow2 planning for every shape (single strips included)
     engine.set_option("f2w", 2)
-    for C in (32, 16):   # 32-row chunks (automatic) and 16 (option C)
+    for C, hl in ((32, 0), (16, 0), (32, 1)):   # 32- and 16-row chunks; 32 with half-chunk LDS links
         engine.set_option("C", C)
+        engine.set_option("f3hl", hl)
         for prm in (engine.Params(), engine.Params(2, -3, 4, 4), engine.Params(1, 0, 0, 0)):
             op = oracle_mod.Params(prm.match, prm.mismatch, prm.gap_init, prm.gap_ext)
             exp = [oracle_mod.score_linear(a, b, op) for a, b in pairs]
@@ -67,6 +68,7 @@ def test_flow3_ragged(engine, oracle_mod):
                 got.append(engine.score(a, b, prm))
                 st = engine.last_stats()
                 assert st["mode"] == 5 and st["variant"] & 64 and st["variant"] & 16 and st["C"] == C, st
+                assert bool(st["variant"] & 512) == bool(hl), st
             assert got == exp, (prm, C)
             assert engine.score_batch(pairs, prm) == exp, (prm, C)
             for blocks in (1, 2, 3):
@@ -74,6 +76,7 @@ def test_flow3_ragged(engine, oracle_mod):
                 assert engine.score_batch(pairs, prm) == exp, (prm, blocks, C)
             engine.set_option("blocks", 0)
     engine.set_option("C", 0)
+    engine.set_option("f3hl", 0)
 
 
 def test_flow3_matches_flow2(engine):
@@ -116,13 +119,18 @@ def test_flow3_config_c2(engine, golden):
     arena = torch.from_numpy(np.concatenate([a, b])).cuda()
     score = torch.full((1,), -1, dtype=torch.int32, device="cuda")
     s = torch.cuda.current_stream()
-    for _ in range(3):
-        engine.score_batch_device(arena.data_ptr(), [0], [N], [N], [N], score.data_ptr(), flags=1,
-                                  stream=s.cuda_stream)
-        engine.stream_status(s.cuda_stream)
-        st = engine.last_stats()
-        assert st["mode"] == 5 and st["variant"] & 64 and not st["variant"] & 2, st
-        assert score.item() == c["score"]
+    try:
+        for hl in (0, 1, 0):   # the default chunks, then 32-row chunks with half-chunk LDS links
+            engine.set_option("f3hl", hl)
+            engine.score_batch_device(arena.data_ptr(), [0], [N], [N], [N], score.data_ptr(), flags=1,
+                                      stream=s.cuda_stream)
+            engine.stream_status(s.cuda_stream)
+            st = engine.last_stats()
+            assert st["mode"] == 5 and st["variant"] & 64 and not st["variant"] & 2, st
+            assert bool(st["variant"] & 512) == bool(hl), st
+            assert score.item() == c["score"]
+    finally:
+        engine.set_option("f3hl", 0)
 
 
 # ---- ring mode (sw_flow3.hip sw_flow3r_kernel: streamed row codes, group edges through

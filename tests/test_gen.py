@@ -14,15 +14,15 @@ def test_flow3_loops_in_sync():
 
 def test_flow3_census_fast_path():
     """The staged chunk loops' fast path (tools/flow3_census.py): at most 10 SALU and 4 s_nop per
-    chunk in every role, no hazard s_nop at all, and at most 30 VALU per chunk beyond the 9 per
+    chunk in every role, no hazard s_nop at all, and at most 32 VALU per chunk beyond the 9 per
     step of the W2 body (score perms and hand-off work included; profiles/r04_flow3_census.txt)."""
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     import flow3_census
     rows = [flow3_census.census(sig, body) for sig, body in
             flow3_census.blocks(os.path.join(flow3_census.CSRC, "sw_flow3_loops.inc"))]
-    assert len(rows) == 12
+    assert len(rows) == 18   # (C, half-chunk links) in (32, 0), (16, 0), (32, 1) x 6 roles
     for r in rows:
         p = r["per_chunk"]
         assert p["salu"] <= 10 and p["s_nop"] <= 4, r
         assert p["s_nop"] == 0, r
-        assert p["extra_valu"] <= 30, r
+        assert p["extra_valu"] <= 32, r

@@ -77,15 +77,22 @@ def granule(a, rows):
     a("buffer_store_dwordx2 v[100:101], v106, %[rsrc], 0 offen sc1")
 
 
-def gen_role(IN, OUT_, spec=0, halfpub=True, C=32):
-    """The staged loop of one strip role at C-row chunks (C = 32 or 16)."""
+def gen_role(IN, OUT_, spec=0, halfpub=True, C=32, hl=False):
+    """The staged loop of one strip role at C-row chunks (C = 32 or 16).  hl: the LDS links
+    hand off every half chunk (C = 32): the producer publishes its newest 16 rows at mid-chunk
+    too, the consumer starts a chunk once its first 16 rows are in and takes the other 16 at
+    mid-chunk (into lanes 0..15 of the I/O register, where the chunk-top rows 16..31 have
+    rotated), so a link lags 63 + 16 steps at C = 32's per-chunk work.  Progress words count
+    rows available - H (H = C/2 with hl, else C); the consumer's word counts rows consumed + R."""
     L = []
     a = L.append
     lds_in, lds_out, gran = IN == "lds", OUT_ == "lds", OUT_ == "gran"
+    H = C // 2 if hl else C
     nd = C // 4                         # row-code dwords per chunk
     ncr = nd // 4                       # their 16-B LDS reads
     nw = 2 if lds_out else 0            # LDS writes of a chunk's publish (ring + mirror in one, the word)
     grows = C // 2 if halfpub else C    # rows per granule publish
+    assert not hl or (C == 32 and spec == 4)
     # ---- entry (s_nop 4: the "s" operands may be fresh from v_readfirstlane, and buffer
     # instructions read them as descriptors: 5 wait states)
     a("s_nop 4")
@@ -101,11 +108,14 @@ def gen_role(IN, OUT_, spec=0, halfpub=True, C=32):
     a("s_mov_b32 s46, 0")
     a(f"s_movk_i32 s44, {R}")            # consumer word seen: 0 rows consumed (+ R)
     if lds_out:
-        a(f"v_mov_b32 v97, {-64 - C}")   # producer word at chunk 0: k0 - 64 rows out, minus C
+        a(f"v_mov_b32 v97, {-64 - H}")   # producer word at chunk 0: k0 - 64 rows out, minus H
         a("v_add_u32 v96, s41, %[lout]")
     if lds_in:
-        a(f"v_mov_b32 v98, {R + C}")     # consumer word after chunk 0: C rows consumed (+ R)
+        a(f"v_mov_b32 v98, {R + H}")     # consumer word after chunk 0's top: H rows consumed (+ R)
         a("v_add_u32 v95, s41, %[lin]")
+        if hl:
+            a("s_movk_i32 s50, 0xffff")  # lanes 0..15: the mid-chunk inflow rows
+            a("s_mov_b32 s51, 0")
     if gran:
         a("v_mov_b32 v105, %[lrow]")
     for q in range(ncr):
@@ -151,9 +161,29 @@ def gen_role(IN, OUT_, spec=0, halfpub=True, C=32):
         spec_at = ng - spec // 4 if spec else None
         for u in range(ng):
             if spec and u == spec_at:
-                book(a, p, lds_in, lds_out, C)
+                book(a, p, lds_in, lds_out, C, H)
                 a("ds_read_b32 v93, %[pin]")
                 a("ds_read_b32 v92, v95")
+            if hl and lds_in and u == ng // 2 - 1:
+                # the second half's rows, read 4 steps ahead behind the producer's word
+                a("ds_read_b32 v93, %[pin]")
+                a(f"ds_read_b32 v102, v95 offset:{4 * H}")
+            if hl and u == ng // 2:
+                # ---- mid-chunk: the newest 16 outflow rows out, the chunk's other 16 rows in
+                if lds_out:
+                    a(f"v_add_u32 v103, {4 * H}, v96")
+                    a(f"v_add_u32 v97, {H}, v97")
+                    a(f"ds_write2st64_b32 v103, v64, v64 offset1:{R * 4 // 256}")
+                    a("ds_write_b32 %[pout], v97")
+                if lds_in:
+                    a(f"s_waitcnt lgkmcnt({1 + (2 if lds_out else 0)})")
+                    a("v_readfirstlane_b32 s43, v93")
+                    a(f"s_add_u32 s52, s40, {H}")
+                    a("s_cmp_lt_i32 s43, s52")
+                    a(f"s_cbranch_scc1 L_mid{p}_%=")
+                    a(f"L_midr{p}_%=:")
+                    a(f"s_waitcnt lgkmcnt({2 if lds_out else 0})")
+                    a("v_cndmask_b32_e64 v64, v64, v102, s[50:51]")
             a(f"v_perm_b32 v72, %[pA], %[k80], v{cur + u}")
             a(f"v_perm_b32 v73, %[pB], %[k80], v{cur + u}")
             for b in range(4):
@@ -162,7 +192,7 @@ def gen_role(IN, OUT_, spec=0, halfpub=True, C=32):
             if gran and halfpub and u == ng // 2 - 1:
                 granule(a, grows)
         if not spec:
-            book(a, p, lds_in, lds_out, C)
+            book(a, p, lds_in, lds_out, C, H)
     a("s_cmp_lt_i32 s40, %[end]")
     a("s_cbranch_scc1 L_loop_%=")
     # ---- exit: the last chunk's outflow, then every row is out
@@ -184,6 +214,9 @@ def gen_role(IN, OUT_, spec=0, halfpub=True, C=32):
     if lds_in:
         for p in (0, 1):
             slow_wait(a, f"L_in{p}_%=", f"L_inr{p}_%=", "v93", "%[pin]", "s43", reread="ds_read_b32 v92, v95")
+            if hl:
+                slow_wait(a, f"L_mid{p}_%=", f"L_midr{p}_%=", "v93", "%[pin]", "s43",
+                          reread=f"ds_read_b32 v102, v95 offset:{4 * H}", target="s52")
     if lds_out:
         slow_wait(a, "L_bp0_%=", "L_bpr0_%=", "v99", "%[qnx]", "s44")
         slow_wait(a, "L_bpx_%=", "L_bpxr_%=", "v99", "%[qnx]", "s44")
@@ -191,14 +224,16 @@ def gen_role(IN, OUT_, spec=0, halfpub=True, C=32):
     return L
 
 
-def book(a, p, lds_in, lds_out, C=32):
-    """Advance k0, the ring offset and the words to the next chunk."""
+def book(a, p, lds_in, lds_out, C=32, H=None):
+    """Advance k0, the ring offset and the words to the next chunk (H: rows a half-chunk
+    publish already added to the producer word)."""
+    H = C if H is None else H
     a(f"s_add_i32 s40, s40, {C}")
     a(f"s_add_u32 s41, s41, {4 * C:#x}")
     a(f"s_and_b32 s41, s41, {(R - 1) * 4:#x}")
     if lds_out:
         a("v_add_u32 v96, s41, %[lout]")
-        a(f"v_add_u32 v97, {C}, v97")
+        a(f"v_add_u32 v97, {C if H == C else C - H}, v97")
     if lds_in:
         a("v_add_u32 v95, s41, %[lin]")
         a(f"v_add_u32 v98, {C}, v98")
@@ -206,9 +241,10 @@ def book(a, p, lds_in, lds_out, C=32):
         a(f"v_add_u32 v94, {2 * C}, v94")
 
 
-def slow_wait(a, label, resume, vreg, addr, sreg, reread=None):
-    """Re-read a progress word until it reaches s40 (k0), then resume; after the
-    deadline (or once failed) give up: s45 = 1 and the kernel reports ERR_TIMEOUT."""
+def slow_wait(a, label, resume, vreg, addr, sreg, reread=None, target="s40"):
+    """Re-read a progress word until it reaches `target` (k0, or k0 + 16 at a half-chunk
+    link's mid-chunk), then resume; after the deadline (or once failed) give up: s45 = 1 and
+    the kernel reports ERR_TIMEOUT."""
     a(f"{label}:")
     a("s_add_u32 s46, s46, 1")
     a("s_cmp_lg_u32 s45, 0")
@@ -220,7 +256,7 @@ def slow_wait(a, label, resume, vreg, addr, sreg, reread=None):
     a("s_memrealtime s[48:49]")
     a("s_waitcnt lgkmcnt(0)")
     a(f"v_readfirstlane_b32 {sreg}, {vreg}")
-    a(f"s_cmp_ge_i32 {sreg}, s40")
+    a(f"s_cmp_ge_i32 {sreg}, {target}")
     a(f"s_cbranch_scc1 {resume}")
     a("s_sub_u32 s48, s48, %[dlo]")
     a("s_subb_u32 s49, s49, %[dhi]")
@@ -233,22 +269,22 @@ def slow_wait(a, label, resume, vreg, addr, sreg, reread=None):
     a(f"s_branch {resume}")
 
 
-CLOBBERS = ['"v%d"' % r for r in range(64, 107) if r not in (75, 102, 103, 104)] + ['"s%d"' % r for r in range(40, 50) if r != 42 and r != 47] \
-    + ['"scc"', '"vcc"', '"memory"']
+CLOBBERS = ['"v%d"' % r for r in range(64, 107) if r not in (75, 104)] + \
+    ['"s%d"' % r for r in range(40, 53) if r != 42 and r != 47] + ['"scc"', '"vcc"', '"memory"']
 
 
 def emit(spec=0, halfpub=True):
     out = ["// GENERATED by tools/gen_flow3.py -- do not edit.  The flow3 chunk loops (sw_flow3.hip):",
-           "// one inline-asm block per (chunk rows C, strip role), R = %d ring rows, SPEC = %d, HALFPUB = %d."
+           "// one inline-asm block per (chunk rows C, half-chunk LDS links HL, strip role), R = %d ring rows, SPEC = %d, HALFPUB = %d."
            % (R, spec, halfpub),
            "// Operands: see F3Loop in sw_flow3.hip; fixed registers: tools/gen_flow3.py.",
            "#pragma once", ""]
-    for C in (32, 16):
+    for C, hl in ((32, 0), (16, 0), (32, 1)):
         for IN in ROLES_IN:
             for OUT_ in ROLES_OUT:
-                body = gen_role(IN, OUT_, spec, halfpub, C)
-                out.append("template <> __device__ __forceinline__ F3Res f3_loop<%d, F3_%s, F3_%s>(const F3Loop& x) {"
-                           % (C, IN.upper(), OUT_.upper()))
+                body = gen_role(IN, OUT_, spec, halfpub, C, bool(hl))
+                out.append("template <> __device__ __forceinline__ F3Res f3_loop<%d, %d, F3_%s, F3_%s>(const F3Loop& x) {"
+                           % (C, hl, IN.upper(), OUT_.upper()))
                 out.append("    F3Res r;")
                 out.append("    asm volatile(")
                 for line in body:
