@@ -134,7 +134,11 @@ def gen_role(IN, OUT_, spec=0, halfpub=True, C=32, hl=False):
             a("ds_read_b32 v92, v95")
         if lds_out:
             if p == 0:   # back-pressure for this chunk's and the next chunk's publish
-                a("s_cmp_lt_i32 s44, s40")
+                if hl:   # (whose mid-chunk write-ahead lanes reach 16 rows further)
+                    a(f"s_add_u32 s52, s40, {H}")
+                    a("s_cmp_lt_i32 s44, s52")
+                else:
+                    a("s_cmp_lt_i32 s44, s40")
                 a(f"s_cbranch_scc1 L_bp{p}_%=")
                 a(f"L_bpr{p}_%=:")
             a(f"ds_write2st64_b32 v96, v64, v64 offset1:{R * 4 // 256}")   # the row and its mirror copy
@@ -218,7 +222,7 @@ def gen_role(IN, OUT_, spec=0, halfpub=True, C=32, hl=False):
                 slow_wait(a, f"L_mid{p}_%=", f"L_midr{p}_%=", "v93", "%[pin]", "s43",
                           reread=f"ds_read_b32 v102, v95 offset:{4 * H}", target="s52")
     if lds_out:
-        slow_wait(a, "L_bp0_%=", "L_bpr0_%=", "v99", "%[qnx]", "s44")
+        slow_wait(a, "L_bp0_%=", "L_bpr0_%=", "v99", "%[qnx]", "s44", target="s52" if hl else "s40")
         slow_wait(a, "L_bpx_%=", "L_bpxr_%=", "v99", "%[qnx]", "s44")
     a("L_done_%=:")
     return L
