@@ -182,7 +182,8 @@ def gen_role(IN, OUT_, spec=0, halfpub=True, C=32, hl=False):
                 if lds_in:
                     a(f"s_waitcnt lgkmcnt({1 + (2 if lds_out else 0)})")
                     a("v_readfirstlane_b32 s43, v93")
-                    a(f"s_add_u32 s52, s40, {H}")
+                    if not (lds_out and p == 0):   # (the chunk top's back-pressure check set s52 = k0 + H)
+                        a(f"s_add_u32 s52, s40, {H}")
                     a("s_cmp_lt_i32 s43, s52")
                     a(f"s_cbranch_scc1 L_mid{p}_%=")
                     a(f"L_midr{p}_%=:")
