@@ -82,7 +82,10 @@ def gen_role(IN, OUT_, spec=0, halfpub=True, C=32, hl=False):
     hand off every half chunk (C = 32): the producer publishes its newest 16 rows at mid-chunk
     too, the consumer starts a chunk once its first 16 rows are in and takes the other 16 at
     mid-chunk (into lanes 0..15 of the I/O register, where the chunk-top rows 16..31 have
-    rotated), so a link lags 63 + 16 steps at C = 32's per-chunk work.  Progress words count
+    rotated), so a link lags 63 + 16 steps at C = 32's per-chunk work.  At mid-chunk only lanes
+    48..63 hold outflow (the chunk top replaced the whole IO register, so lanes 32..47 hold its
+    inflow): the mid publish sends lanes 32..47 32 rows on (%[lmid]), onto write-ahead slots,
+    never over rows the top already published.  Progress words count
     rows available - H (H = C/2 with hl, else C); the consumer's word counts rows consumed + R."""
     L = []
     a = L.append
@@ -114,7 +117,7 @@ def gen_role(IN, OUT_, spec=0, halfpub=True, C=32, hl=False):
         a(f"v_mov_b32 v98, {R + H}")     # consumer word after chunk 0's top: H rows consumed (+ R)
         a("v_add_u32 v95, s41, %[lin]")
         if hl:
-            a("s_movk_i32 s50, 0xffff")  # lanes 0..15: the mid-chunk inflow rows
+            a("s_mov_b32 s50, 0xffff")   # lanes 0..15: the mid-chunk inflow rows
             a("s_mov_b32 s51, 0")
     if gran:
         a("v_mov_b32 v105, %[lrow]")
@@ -175,7 +178,7 @@ def gen_role(IN, OUT_, spec=0, halfpub=True, C=32, hl=False):
             if hl and u == ng // 2:
                 # ---- mid-chunk: the newest 16 outflow rows out, the chunk's other 16 rows in
                 if lds_out:
-                    a(f"v_add_u32 v103, {4 * H}, v96")
+                    a("v_add_u32 v103, %[lmid], v96")   # lanes 32..47 (the chunk top's inflow) 32 rows on
                     a(f"v_add_u32 v97, {H}, v97")
                     a(f"ds_write2st64_b32 v103, v64, v64 offset1:{R * 4 // 256}")
                     a("ds_write_b32 %[pout], v97")
@@ -299,7 +302,7 @@ def emit(spec=0, halfpub=True):
                 out.append('          [code] "v"(x.code), [lin] "v"(x.lin), [lout] "v"(x.lout), [pin] "v"(x.pin),')
                 out.append('          [pout] "v"(x.pout), [qme] "v"(x.qme), [qnx] "v"(x.qnx), [end] "s"(x.end),')
                 out.append('          [dlo] "s"(x.dlo), [dhi] "s"(x.dhi), [rsrc] "s"(x.rsrc), [ek] "s"(x.ek),')
-                out.append('          [lrow] "v"(x.lrow), [m48] "s"(x.m48)')
+                out.append('          [lrow] "v"(x.lrow), [m48] "s"(x.m48), [lmid] "v"(x.lmid)')
                 out.append("        : " + ", ".join(CLOBBERS) + ");")
                 out.append("    return r;")
                 out.append("}")
