@@ -64,7 +64,7 @@ Params g_params;
 
 std::atomic<long long> g_opt_W{0}, g_opt_C{0}, g_opt_bytes{0}, g_opt_timeout{30}, g_opt_blocks{0}, g_opt_orient{0},
     g_opt_mode{-1}, g_opt_trace{0}, g_opt_duo_f16{1}, g_opt_f2stream{0}, g_opt_ring{-1}, g_opt_ring_rows{4096}, g_opt_f2_wgs{0}, g_opt_f2w{0}, g_opt_f2pwg{-1},
-    g_opt_linear{-1}, g_opt_f3{1}, g_opt_slab_plain{0}, g_opt_duo_lds{1}, g_opt_duo_tab{1}, g_opt_duo_roles{1}, g_opt_f3hl{0};
+    g_opt_linear{-1}, g_opt_f3{1}, g_opt_slab_plain{0}, g_opt_duo_lds{1}, g_opt_duo_tab{1}, g_opt_duo_roles{1}, g_opt_f3hl{1};
 
 // Longest sequence the engine takes: granule buffers of m rows keep m * 16 in the
 // 32-bit record count of a buffer resource (sw_device.h linear_edge).
@@ -452,9 +452,9 @@ int finalize_mode(Job& job, const Params& prm, int cus) {
             // ring mode (one pair of many groups per CU, C5): throughput-bound, so 64-row chunks
             // (half the per-chunk work per step) beat the shorter hand-off lag of 32 (C5 249 -> 220 ms)
             if (job.ring && g_opt_C.load() == 0) job.C = 64;
-            // the staged two-column kernel on flow3 (C2): 16-row chunks, whose shorter hand-off lag
-            // (63 + 16 steps a strip) outweighs their per-chunk work there (2.70 -> 2.65 ms)
-            // (option f3hl: 32-row chunks whose in-workgroup links hand off every half chunk instead)
+            // the staged two-column kernel on flow3 (C2): 32-row chunks whose in-workgroup links hand
+            // off every half chunk (option f3hl, default 1: C = 32's per-chunk work at a 63 + 16-step
+            // lag, 2.645 -> 2.600 ms); with f3hl = 0, 16-row chunks (2.70 -> 2.65 ms against plain 32)
             if (!job.ring && !job.f2_stream && !job.slab && job.f2w2 && g_opt_C.load() == 0 && g_opt_f3.load() != 0 &&
                 g_opt_f3hl.load() == 0 && flow3_fits(max_m, 16))
                 job.C = 16;

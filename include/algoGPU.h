@@ -192,6 +192,8 @@ void sw_db_close(sw_db* db);
  *   "f3"       1 = (default) a two-column linear-gap flow2 launch runs the flow3 kernel
  *              (hand-scheduled chunk loops): staged codes at C = 32 / 16 (C2), ring edges at
  *              C = 64 (C5); 0 = the compiled flow2 kernel
+ *   "f3hl"     1 = (default) flow3 staged launches run 32-row chunks whose in-workgroup links
+ *              hand off every half chunk (16 rows); 0 = whole-chunk links at C = 16 (auto C)
  *   "duo_lds"  1 = (default) duo batches at C = 64 hand strip edges on in LDS when a round's
  *              rows fit (m <= 16384 linear-gap step, 8192 affine), 0 = through HBM granules
  *   "duo_roles" 1 = (default) the two duo LDS workgroups of a CU take complementary strip roles
@@ -220,7 +222,8 @@ typedef struct {
                                bit 4: flow2 two columns per lane; bit 5: flow2 pair per workgroup;
                                bit 6: the flow3 kernel (sw_flow3.hip);
                                bit 7: duo strip hand-offs in LDS (no boundary buffers);
-                               bit 8: duo row codes from an LDS table */
+                               bit 8: duo row codes from an LDS table;
+                               bit 9: flow3 half-chunk LDS links (option f3hl) */
 } sw_stats;
 int sw_last_stats(sw_stats* out);
 

@@ -39,6 +39,7 @@ def _defaults(engine):
         engine.set_option("mode", -1)
         engine.set_option("linear", -1)
         engine.set_option("f3", 1)
+        engine.set_option("f3hl", 1)
     reset()
     yield
     reset()
@@ -76,7 +77,6 @@ def test_flow3_ragged(engine, oracle_mod):
                 assert engine.score_batch(pairs, prm) == exp, (prm, blocks, C)
             engine.set_option("blocks", 0)
     engine.set_option("C", 0)
-    engine.set_option("f3hl", 0)
 
 
 def test_flow3_matches_flow2(engine):
@@ -120,17 +120,17 @@ def test_flow3_config_c2(engine, golden):
     score = torch.full((1,), -1, dtype=torch.int32, device="cuda")
     s = torch.cuda.current_stream()
     try:
-        for hl in (0, 1, 0):   # the default chunks, then 32-row chunks with half-chunk LDS links
+        for hl in (1, 0, 1):   # the default (32-row chunks, half-chunk LDS links), then 16-row chunks
             engine.set_option("f3hl", hl)
             engine.score_batch_device(arena.data_ptr(), [0], [N], [N], [N], score.data_ptr(), flags=1,
                                       stream=s.cuda_stream)
             engine.stream_status(s.cuda_stream)
             st = engine.last_stats()
             assert st["mode"] == 5 and st["variant"] & 64 and not st["variant"] & 2, st
-            assert bool(st["variant"] & 512) == bool(hl), st
+            assert bool(st["variant"] & 512) == bool(hl) and st["C"] == (32 if hl else 16), st
             assert score.item() == c["score"]
     finally:
-        engine.set_option("f3hl", 0)
+        engine.set_option("f3hl", 1)
 
 
 # ---- ring mode (sw_flow3.hip sw_flow3r_kernel: streamed row codes, group edges through
