@@ -64,7 +64,8 @@ Params g_params;
 
 std::atomic<long long> g_opt_W{0}, g_opt_C{0}, g_opt_bytes{0}, g_opt_timeout{30}, g_opt_blocks{0}, g_opt_orient{0},
     g_opt_mode{-1}, g_opt_trace{0}, g_opt_duo_f16{1}, g_opt_f2stream{0}, g_opt_ring{-1}, g_opt_ring_rows{4096}, g_opt_f2_wgs{0}, g_opt_f2w{0}, g_opt_f2pwg{-1},
-    g_opt_linear{-1}, g_opt_f3{1}, g_opt_slab_plain{0}, g_opt_duo_lds{1}, g_opt_duo_tab{1}, g_opt_duo_roles{1}, g_opt_f3hl{1};
+    g_opt_linear{-1}, g_opt_f3{1}, g_opt_slab_plain{0}, g_opt_duo_lds{1}, g_opt_duo_tab{1}, g_opt_duo_roles{1}, g_opt_f3hl{1},
+    g_opt_f3rhl{0};
 
 // Longest sequence the engine takes: granule buffers of m rows keep m * 16 in the
 // 32-bit record count of a buffer resource (sw_device.h linear_edge).
@@ -698,6 +699,7 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
         probe.f2_stream = true;
         probe.f2_lin = f2_lin;
         probe.f2_w2 = job.f2w2;
+        probe.f3_hl = use_f3 && job.C == 64 && g_opt_f3rhl.load() != 0;
         int fit = 0;
         for (;; --f2_wgs) {
             probe.f2_wgs = f2_wgs;
@@ -768,7 +770,8 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
     // the staged two-column linear-gap kernel with hand-scheduled chunk loops (sw_flow3.hip), unless
     // option f3 = 0: C2
     cfg.f3 = use_f3;
-    cfg.f3_hl = use_f3 && !job.ring && job.C == 32 && g_opt_f3hl.load() != 0;
+    cfg.f3_hl = use_f3 && ((!job.ring && job.C == 32 && g_opt_f3hl.load() != 0) ||
+                           (job.ring && job.C == 64 && g_opt_f3rhl.load() != 0));
     cfg.duo_wrap = duo_wrap;
     cfg.duo_tab = duo_tab;
     if (cfg.f2_w2 && job.C == 16 && !use_f3) {
@@ -1641,6 +1644,9 @@ int sw_set_option(const char* key, long long v) {
     } else if (k == "f3hl") {   // 1: flow3 staged launches at C = 32 with half-chunk in-workgroup links (auto C: 32)
         if (v < 0 || v > 1) return -1;
         g_opt_f3hl = v;
+    } else if (k == "f3rhl") {   // 1: flow3 ring launches at C = 64 with half-chunk in-workgroup links
+        if (v < 0 || v > 1) return -1;
+        g_opt_f3rhl = v;
     } else if (k == "duo_roles") {   // 1 (default): duo strip roles complementary per SIMD across a CU's workgroups
         if (v < 0 || v > 1) return -1;
         g_opt_duo_roles = v;
@@ -1689,6 +1695,7 @@ long long sw_get_option(const char* key) {
     if (k == "duo_tab") return g_opt_duo_tab;
     if (k == "duo_roles") return g_opt_duo_roles;
     if (k == "f3hl") return g_opt_f3hl;
+    if (k == "f3rhl") return g_opt_f3rhl;
     return -1;
 }
 

@@ -194,6 +194,8 @@ void sw_db_close(sw_db* db);
  *              C = 64 (C5); 0 = the compiled flow2 kernel
  *   "f3hl"     1 = (default) flow3 staged launches run 32-row chunks whose in-workgroup links
  *              hand off every half chunk (16 rows); 0 = whole-chunk links at C = 16 (auto C)
+ *   "f3rhl"    1 = flow3 ring launches (C = 64) with half-chunk in-workgroup links (32 rows),
+ *              0 = (default) whole-chunk links (measured faster on C5)
  *   "duo_lds"  1 = (default) duo batches at C = 64 hand strip edges on in LDS when a round's
  *              rows fit (m <= 16384 linear-gap step, 8192 affine), 0 = through HBM granules
  *   "duo_roles" 1 = (default) the two duo LDS workgroups of a CU take complementary strip roles

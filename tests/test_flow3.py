@@ -148,6 +148,7 @@ def _ring_reset(engine):
     engine.set_option("ring", -1)
     engine.set_option("ring_rows", 4096)
     engine.set_option("blocks", 0)
+    engine.set_option("f3rhl", 0)
 
 
 def test_flow3_ring_parity(engine, oracle_mod, _ring_reset):
@@ -160,8 +161,10 @@ def test_flow3_ring_parity(engine, oracle_mod, _ring_reset):
     for prm in (engine.Params(), engine.Params(2, -3, 4, 4), engine.Params(1, 0, 0, 0)):
         op = oracle_mod.Params(prm.match, prm.mismatch, prm.gap_init, prm.gap_ext)
         exp = [oracle_mod.score_linear(a, b, op) for a, b in pairs]
-        for C in (64, 32):   # 64-row chunks (automatic in ring mode) and 32 (option C)
+        # 64-row chunks (automatic in ring mode), 32 (option C), 64 with half-chunk LDS links
+        for C, hl in ((64, 0), (32, 0), (64, 1)):
             engine.set_option("C", 0 if C == 64 else C)
+            engine.set_option("f3rhl", hl)
             for blocks, rows in ((0, 4096), (1, 512), (2, 512), (3, 1024), (7, 512)):
                 _ring_opts(engine, blocks, rows)
                 got = []
@@ -171,6 +174,7 @@ def test_flow3_ring_parity(engine, oracle_mod, _ring_reset):
                     groups = (((len(a) - 2 + 125) // 126 if len(a) > 128 else 1) + 3) // 4
                     if groups > 1:
                         assert st["variant"] & 64 and st["variant"] & 4 and st["C"] == C, st
+                        assert bool(st["variant"] & 512) == bool(hl), st
                 assert got == exp, (prm, C, blocks, rows)
         engine.set_option("C", 0)
 
@@ -186,9 +190,10 @@ def test_flow3_ring_matches_flow2(engine, _ring_reset):
     engine.set_option("ring", 1)
     out = []
     try:
-        for f3, C in ((1, 0), (1, 32), (0, 0)):
+        for f3, C, hl in ((1, 0, 0), (1, 32, 0), (1, 0, 1), (0, 0, 0)):
             engine.set_option("f3", f3)
             engine.set_option("C", C)
+            engine.set_option("f3rhl", hl)
             engine.score_batch_device(arena.data_ptr(), [0], [N], [N], [N], score.data_ptr(), flags=1,
                                       stream=s.cuda_stream)
             engine.stream_status(s.cuda_stream)
@@ -198,4 +203,4 @@ def test_flow3_ring_matches_flow2(engine, _ring_reset):
     finally:
         engine.set_option("f3", 1)
         engine.set_option("C", 0)
-    assert out[0] == out[1] == out[2] > 0
+    assert out[0] == out[1] == out[2] == out[3] > 0

@@ -360,13 +360,21 @@ def ring_gin_check(a, C=64):
     a("s_cmp_lg_u64 s[50:51], 0")
 
 
-def gen_role_ring(IN, OUT_, C=64):
+def gen_role_ring(IN, OUT_, C=64, hl=False):
     """The ring-mode loop of one strip role at C-row chunks (64, or 32: half the hand-off
-    lag).  The loop body is two chunks; the code ring is refilled 64 rows per body."""
+    lag).  The loop body is two chunks; the code ring is refilled 64 rows per body.
+    hl (C = 64): half-chunk LDS links as in gen_role: the producer also publishes its newest
+    32 rows (lanes 32..63) at mid-chunk, lanes 0..31 (the chunk top's inflow) onto the
+    write-ahead slots 64 rows on (%[lmid] from the ring offset of chunk k0 + 64); the consumer
+    starts a chunk on its first 32 rows and merges the other 32 into lanes 0..31 at mid-chunk.
+    Words count rows available - 32; the back-pressure floor is k0 + 64 (the next mid-chunk's
+    write-ahead)."""
     L = []
     a = L.append
     lds_in, lds_out = IN == "lds", OUT_ == "lds"
     gin, gout = IN == "gran", OUT_ == "gran"
+    assert not hl or C == 64
+    H = C // 2 if hl else C
     ncr = C // 16                                      # 16-B code reads per chunk
     # ---- entry (s_nop 4: descriptor operands may be fresh from v_readfirstlane)
     a("s_nop 4")
@@ -390,10 +398,10 @@ def gen_role_ring(IN, OUT_, C=64):
     a("s_mov_b32 s52, 0")
     if lds_out:
         # producer word at chunk 0: rows available (< k0 - 63) - C, one row conservative
-        a(f"v_mov_b32 v90, {(-64 - C) & 0xffffffff:#x}")
+        a(f"v_mov_b32 v90, {(-64 - H) & 0xffffffff:#x}")
         a("v_add_u32 v89, s41, %[lout]")
     if lds_in:
-        a(f"v_mov_b32 v91, {RR + C}")               # consumer word after chunk 0: C consumed (+ R)
+        a(f"v_mov_b32 v91, {RR + H}")               # consumer word after chunk 0: H consumed (+ R)
         a("v_add_u32 v88, s42, %[lin]")
     if gout:
         a("v_mov_b32 v98, %[gooff]")
@@ -416,7 +424,11 @@ def gen_role_ring(IN, OUT_, C=64):
         # into slots of the next chunk's rows or the ring's slack, never read before rewritten)
         if lds_out:
             if p == 0:
-                a("s_cmp_lt_i32 s44, s40")
+                if hl:
+                    a("s_add_u32 s54, s40, 64")
+                    a("s_cmp_lt_i32 s44, s54")
+                else:
+                    a("s_cmp_lt_i32 s44, s40")
                 a(f"s_cbranch_scc1 L_bp{p}_%=")
                 a(f"L_bpr{p}_%=:")
             a("ds_write_b32 v89, v40")
@@ -502,6 +514,28 @@ def gen_role_ring(IN, OUT_, C=64):
             a(f"s_waitcnt lgkmcnt({len(lds)})")
         # 8. C steps, C/4 groups of 4 rows
         for u in range(C // 4):
+            if hl and lds_in and u == C // 8 - 1:
+                # the second half's rows, read 4 steps ahead behind the producer's word
+                a("ds_read_b32 v86, %[pin]")
+                a(f"ds_read_b32 v102, v88 offset:{4 * H}")
+            if hl and u == C // 8:
+                # ---- mid-chunk: the newest 32 outflow rows out, the chunk's other 32 rows in
+                if lds_out:
+                    a(f"s_add_u32 s55, s41, {4 * C:#x}")
+                    a(f"s_and_b32 s55, s55, {(RR - 1) * 4:#x}")
+                    a("v_add_u32 v96, s55, %[lmid]")
+                    a(f"v_add_u32 v90, {H}, v90")
+                    a("ds_write_b32 v96, v40")
+                    a("ds_write_b32 %[pout], v90")
+                if lds_in:
+                    a(f"s_waitcnt lgkmcnt({1 + (2 if lds_out else 0)})")
+                    a("v_readfirstlane_b32 s43, v86")
+                    a(f"s_add_u32 s54, s40, {H}")
+                    a("s_cmp_lt_i32 s43, s54")
+                    a(f"s_cbranch_scc1 L_mid{p}_%=")
+                    a(f"L_midr{p}_%=:")
+                    a(f"s_waitcnt lgkmcnt({2 if lds_out else 0})")
+                    a("v_cndmask_b32_e64 v40, v102, v40, %[lhi]")
             a(f"v_perm_b32 v48, %[pA], %[k80], v{cur + u}")
             a(f"v_perm_b32 v49, %[pB], %[k80], v{cur + u}")
             for b in range(4):
@@ -515,7 +549,7 @@ def gen_role_ring(IN, OUT_, C=64):
             a(f"s_add_u32 s41, s41, {4 * C:#x}")
             a(f"s_and_b32 s41, s41, {(RR - 1) * 4:#x}")
             a("v_add_u32 v89, s41, %[lout]")
-            a(f"v_add_u32 v90, {C}, v90")
+            a(f"v_add_u32 v90, {C - H if hl else C}, v90")
         if lds_in:
             a(f"s_add_u32 s42, s42, {4 * C:#x}")
             a(f"s_and_b32 s42, s42, {(RR - 1) * 4:#x}")
@@ -551,8 +585,11 @@ def gen_role_ring(IN, OUT_, C=64):
     if lds_in:
         for p in (0, 1):
             slow_wait(a, f"L_in{p}_%=", f"L_inr{p}_%=", "v86", "%[pin]", "s43", reread="ds_read_b32 v84, v88")
+            if hl:
+                slow_wait(a, f"L_mid{p}_%=", f"L_midr{p}_%=", "v86", "%[pin]", "s43",
+                          reread=f"ds_read_b32 v102, v88 offset:{4 * H}", target="s54")
     if lds_out:
-        slow_wait(a, "L_bp0_%=", "L_bpr0_%=", "v92", "%[qnx]", "s44")
+        slow_wait(a, "L_bp0_%=", "L_bpr0_%=", "v92", "%[qnx]", "s44", target="s54" if hl else "s40")
         slow_wait(a, "L_bpx_%=", "L_bpxr_%=", "v92", "%[qnx]", "s44")
     if gout:
         for lab, res in (("L_bpg0_%=", "L_bpgr0_%="), ("L_bpg1_%=", "L_bpgr1_%="), ("L_bpgx_%=", "L_bpgxr_%=")):
@@ -621,14 +658,14 @@ CLOBBERS_RING = ['"v%d"' % r for r in range(40, 108) if r != 51] + \
 
 def emit_ring():
     out = ["// GENERATED by tools/gen_flow3.py -- do not edit.  The flow3 ring-mode chunk loops",
-           "// (sw_flow3.hip sw_flow3r_kernel): one inline-asm block per (chunk rows C, strip role), R = %d." % RR,
+           "// (sw_flow3.hip sw_flow3r_kernel): one inline-asm block per (chunk rows C, half-chunk LDS links HL, strip role), R = %d." % RR,
            "// Operands: see F3RLoop in sw_flow3.hip; fixed registers: tools/gen_flow3.py.",
            "#pragma once", ""]
-    for C in (64, 32):
+    for C, hl in ((64, 0), (32, 0), (64, 1)):
         for IN, OUT_ in [(i, o) for i in ROLES_IN_RING for o in ROLES_OUT]:
-            body = gen_role_ring(IN, OUT_, C)
-            out.append("template <> __device__ __forceinline__ F3Res f3r_loop<%d, F3_%s, F3_%s>(const F3RLoop& x) {"
-                       % (C, IN.upper(), OUT_.upper()))
+            body = gen_role_ring(IN, OUT_, C, bool(hl))
+            out.append("template <> __device__ __forceinline__ F3Res f3r_loop<%d, %d, F3_%s, F3_%s>(const F3RLoop& x) {"
+                       % (C, hl, IN.upper(), OUT_.upper()))
             out.append("    F3Res r;")
             out.append("    asm volatile(")
             for line in body:
@@ -643,7 +680,8 @@ def emit_ring():
             out.append('          [girs] "s"(x.girs), [gioff] "v"(x.gioff), [gipos] "v"(x.gipos), [gimask8] "s"(x.gimask8),')
             out.append('          [ek] "s"(x.ek), [cross] "s"(x.cross), [crv0] "s"(x.crv0), [croff] "v"(x.croff),')
             out.append('          [gors] "s"(x.gors), [gooff] "v"(x.gooff), [gopos] "v"(x.gopos), [gomask8] "s"(x.gomask8),')
-            out.append('          [gorow] "v"(x.gorow), [lhi] "s"(x.lhi), [bpr] "s"(x.bpr), [bpbase] "s"(x.bpbase)')
+            out.append('          [gorow] "v"(x.gorow), [lhi] "s"(x.lhi), [bpr] "s"(x.bpr), [bpbase] "s"(x.bpbase),')
+            out.append('          [lmid] "v"(x.lmid)')
             out.append("        : " + ", ".join(CLOBBERS_RING) + ");")
             out.append("    return r;")
             out.append("}")
