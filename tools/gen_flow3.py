@@ -42,6 +42,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(ROOT, "concurrentproject_amd", "csrc", "sw_flow3_loops.inc")
 
 ROLES_IN = ("none", "lds")
+MID_AHEAD = int(os.environ.get("F3_MIDAHEAD", "1"))   # 4-step groups the mid-chunk inflow read runs ahead
 ROLES_OUT = ("none", "lds", "gran")
 
 
@@ -171,7 +172,7 @@ def gen_role(IN, OUT_, spec=0, halfpub=True, C=32, hl=False):
                 book(a, p, lds_in, lds_out, C, H)
                 a("ds_read_b32 v93, %[pin]")
                 a("ds_read_b32 v92, v95")
-            if hl and lds_in and u == ng // 2 - 1:
+            if hl and lds_in and u == ng // 2 - MID_AHEAD:
                 # the second half's rows, read 4 steps ahead behind the producer's word
                 a("ds_read_b32 v93, %[pin]")
                 a(f"ds_read_b32 v102, v95 offset:{4 * H}")
