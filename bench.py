@@ -74,7 +74,8 @@ def parse():
     ap.add_argument("--pairs-per-gpu", type=int, default=1024)
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU baseline leg")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-extra", action="store_true", help="N=1 auto: skip the extra C3 batch measurement")
+    ap.add_argument("--no-extra", action="store_true", help="N=1 auto: skip the extra C3 / affine / C5 measurements")
+    ap.add_argument("--no-c5", action="store_true", help="N=1 auto: skip the extra C5 (N=2^20) launches")
     ap.add_argument("--W", type=int, default=0)
     ap.add_argument("--C", type=int, default=0)
     ap.add_argument("--mode", type=int, default=-1, help="engine option 'mode' (-1 = automatic plan)")
@@ -251,6 +252,107 @@ def roofline(workload, per_launch_cells, avg_kern_ms, step_ns=None, n=0, m=0, w2
             body_ns = min(r["ns_per_4steps"] for r in rows) / 4
             out["step_body_ns"] = round(body_ns, 3)
             out["issue_path_frac"] = round((m + 63 * strips) * body_ns / (avg_kern_ms * 1e6), 4)
+    return out
+
+
+def kernel_label(st):
+    """What a launch ran, from sw_last_stats (mode + variant bits, sw_engine.hip enqueue):
+    the kernel family, the HIP function it launched (the name rocprof reports), the columns
+    per lane actually computed and the step (the exact linear-gap identity at G_INIT ==
+    G_EXT, DESIGN.md section 2, or the general affine Gotoh step)."""
+    v, mode = st["variant"], st["mode"]
+    lin = bool(v & 8)
+    out = {"W": st["W"]}
+    if mode == 5:
+        ring, w2, f3, hl, aff3 = bool(v & 4), bool(v & 16), bool(v & 64), bool(v & 512), bool(v & 1024)
+        if f3 or aff3:
+            name = ("flow3 ring" if ring else "flow3") + (" affine" if aff3 else "")
+            fn = ("sw_flow3r" if ring else "sw_flow3") + ("a" if aff3 else "") + "_kernel"
+        else:
+            name = "flow2 " + ("pair per workgroup" if v & 32 else "ring" if ring else "streamed" if v & 2 else "staged")
+            fn = "sw_flow2_kernel"
+        if hl:
+            name += ", half-chunk links"
+        out["W"] = 2 if w2 else 1
+    elif mode == 3:
+        name = "duo" + (" LDS hand-offs" if v & 128 else " granules") + (", row-code table" if v & 256 else "") + \
+               (", f16-max3" if v & 1 else "")
+        fn = "sw_duo_lds_kernel" if v & 128 else "sw_duo_kernel"
+        lin = bool(v & 8)
+    else:
+        name = {0: "strip", 1: "pairwg", 2: "chain", 4: "flow"}.get(mode, str(mode))
+        fn = {0: "sw_strip_kernel", 1: "sw_pairwg_kernel", 2: "sw_chain_kernel", 4: "sw_flow_kernel"}.get(mode, "?")
+    out.update(kernel=name, kernel_fn=fn, C=st["C"],
+               step="linear-gap identity (G_INIT == G_EXT, exact)" if lin else "affine (Gotoh E/F)")
+    return out
+
+
+AFFINE_PARAMS = (2, -3, 5, 2)   # G_INIT != G_EXT: the general Gotoh step (goldens C2_affine, C3_affine, C5_affine)
+
+
+def affine_runs(sw, torch, launch, scores, stream, gold, N, steps, params, defaults):
+    """N = 1 extras of the pair workload: the general affine step (G_INIT != G_EXT, params
+    AFFINE_PARAMS) on the C2 pair against its reference-pinned golden, and the same step
+    forced at the default constants (option linear = 0: no linear-gap identity)."""
+    out = {}
+    st_steps = max(3, steps // 2)
+    try:
+        sw.set_params(sw.Params(*AFFINE_PARAMS))
+        at, ak = time_launches(torch, launch, lambda: None, st_steps, 1, stream, None)
+        sw.stream_status(stream.cuda_stream)
+        st = sw.last_stats()
+        g = gold.get("C2_affine", {})
+        out = {"params": list(AFFINE_PARAMS), "ms_per_step": round(at / st_steps * 1e3, 4),
+               "value": round(N * N * st_steps / at / 1e9, 3), "unit": "GCUPS",
+               "kernel_ms_per_launch": round(ak, 4), "kernel_gcups": round(N * N / (ak * 1e-3) / 1e9, 3),
+               "parity": ("ok" if scores[0].item() == g["score"] else "MISMATCH") if g and N == 65536 else "unchecked",
+               "golden": "C2_affine (reference LazySmith built with these constants)", **kernel_label(st),
+               "roofline": roofline("pair_affine", N * N, ak)}
+    finally:
+        sw.set_params(sw.Params(*params))
+    sw.set_option("linear", 0)
+    try:
+        at, ak = time_launches(torch, launch, lambda: None, st_steps, 1, stream, None)
+        sw.stream_status(stream.cuda_stream)
+        ok = ("ok" if scores[0].item() == gold.get("C2", {}).get("score") else "MISMATCH") \
+            if defaults and N == 65536 else "unchecked"
+        out["default_consts_linear0"] = {"kernel_ms_per_launch": round(ak, 4),
+                                         "kernel_gcups": round(N * N / (ak * 1e-3) / 1e9, 3), "parity": ok,
+                                         **kernel_label(sw.last_stats()),
+                                         "note": "option linear=0: the affine step at (1,-1,1,1) on the C2 pair"}
+    finally:
+        sw.set_option("linear", -1)
+    return out
+
+
+def c5_runs(sw, torch, gold, steps):
+    """N = 1 extras: config C5 (one pair N = 2^20, seed 1048576, O(N) device state) with the
+    reference's constants and with AFFINE_PARAMS, each against its golden."""
+    N = 1 << 20
+    a, b = sw.gen_pair(1048576, N)
+    arena = torch.from_numpy(np.concatenate([a, b])).cuda()
+    scores = torch.zeros(1, dtype=torch.int32, device="cuda")
+    stream = torch.cuda.current_stream()
+
+    def launch():
+        sw.score_batch_device(arena.data_ptr(), [0], [N], [N], [N], scores.data_ptr(), flags=1,
+                              stream=stream.cuda_stream)
+    out = {}
+    for key, prm, gk in (("linear", (1, -1, 1, 1), "C5"), ("affine", AFFINE_PARAMS, "C5_affine")):
+        sw.set_params(sw.Params(*prm))
+        try:
+            t, k = time_launches(torch, launch, lambda: None, steps, 1, stream, None)
+            sw.stream_status(stream.cuda_stream)
+            g = gold.get(gk, {})
+            out[key] = {"params": list(prm), "ms_per_step": round(t / steps * 1e3, 3),
+                        "value": round(N * N * steps / t / 1e9, 3), "unit": "GCUPS",
+                        "kernel_ms_per_launch": round(k, 3), "steps": steps,
+                        "parity": ("ok" if scores[0].item() == g["score"] else "MISMATCH") if g else "unchecked",
+                        "score": scores[0].item(), **kernel_label(sw.last_stats()),
+                        "boundary_bytes": sw.last_stats()["boundary_bytes"]}
+        finally:
+            sw.set_params(sw.Params(1, -1, 1, 1))
+    out["workload"] = "C5 single pair N=2^20 (seed 1048576), resident in HBM"
     return out
 
 
@@ -525,6 +627,8 @@ def main():
     slab_ranks = None
 
     extra = None
+    c5 = None
+    affine = None
     step_ns = None
     host_api = None
     parity = "unchecked"
@@ -639,16 +743,11 @@ def main():
         affine = None
         if workload == "pair" and world == 1 and args.workload == "auto" and not args.no_extra and \
                 params[2] == params[3]:
-            sw.set_option("linear", 0)
-            try:
-                at, ak = time_launches(torch, launch, lambda: None, max(3, args.steps // 2), 1, stream, None)
-                sw.stream_status(sptr)
-                ok = ("ok" if scores[0].item() == gold.get("C2", {}).get("score") else "MISMATCH") \
-                    if defaults and N == 65536 else "unchecked"
-                affine = {"kernel_ms_per_launch": round(ak, 4), "kernel_gcups": round(N * N / (ak * 1e-3) / 1e9, 3),
-                          "parity": ok, "note": "option linear=0: the general affine (E, F) step on the C2 pair"}
-            finally:
-                sw.set_option("linear", -1)
+            affine = affine_runs(sw, torch, launch, scores, stream, gold, N, args.steps, params, defaults)
+        c5 = None
+        if workload == "pair" and world == 1 and args.workload == "auto" and not args.no_extra and \
+                not args.no_c5 and defaults and N == 65536:
+            c5 = c5_runs(sw, torch, gold, 2)
         # the batched config measured right after on the same ranks, as an extra key:
         # C3 at N=1, 1024 pairs per GPU sharded + RCCL-gathered at N>1 (C4 at N=8)
         if workload == "pair" and args.workload == "auto" and not args.no_extra:
@@ -663,7 +762,7 @@ def main():
                      "kernel_gcups": round(bcells / (bk * 1e-3) / 1e9, 3),
                      "parity": ("ok" if bsc == ref[:len(bsc)] else "MISMATCH")
                      if defaults and len(ref) >= len(bsc) == 1024 * world else "unchecked",
-                     "kernel": {3: "duo", 1: "pairwg", 5: "flow2"}.get(bst["mode"], bst["mode"]),
+                     **kernel_label(bst),
                      "dtype": "u16x2 (packed, exact: scores < 2^16)" if bst["mode"] == 3 else "int32",
                      "roofline": roofline("batch", bcells, bk, waves_per_simd=resident_waves_per_simd(bst, torch))}
         if extra is not None and world == 1:
@@ -701,10 +800,8 @@ def main():
             "vs_baseline": None,
             "dtype": "u16x2 (packed, exact: scores < 2^16)" if st["mode"] == 3 else "int32",
             "data": "synthetic (uniform ACGT, mt19937_64 seeds as cudaSmithM.cu:200-212), resident in HBM",
-            "config": dict(cfg, params=list(params), W=st["W"], C=st["C"], kernel_items=st["items"],
-                           blocks=st["blocks"], boundary_bytes=st["boundary_bytes"],
-                           kernel={0: "strip", 1: "pairwg", 2: "chain", 3: "duo", 4: "flow",
-                                   5: "flow2"}.get(st["mode"], st["mode"])),
+            "config": dict(cfg, params=list(params), kernel_items=st["items"], blocks=st["blocks"],
+                           boundary_bytes=st["boundary_bytes"], **kernel_label(st)),
             "kernel_ms_per_launch": round(avg_kern_ms, 4),
             "kernel_gcups": round(per_launch_cells / (avg_kern_ms * 1e-3) / 1e9, 3),
             "parity": parity,
@@ -728,6 +825,8 @@ def main():
                                    % (N, "batch_c3" if world == 1 else "batch_c4"))
         if workload != "batch" and affine is not None:
             out["affine_step"] = affine
+        if workload != "batch" and c5 is not None:
+            out["c5"] = c5
         if world == 1 and not args.no_cpu_baseline:
             try:
                 out["cpu_baseline"] = cpu_baseline(workload, cfg["N"], args.cpu_seconds, params)

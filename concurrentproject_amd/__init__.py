@@ -111,6 +111,8 @@ def lib() -> ctypes.CDLL:
     L.sw_score_batch_multi.restype = i
     L.sw_batch_shard.argtypes = [i, i, i, ctypes.POINTER(i), ctypes.POINTER(i)]
     L.sw_batch_shard.restype = i
+    L.sw_batch_gather_plan.argtypes = [i, i, ctypes.POINTER(i), ctypes.POINTER(i)]
+    L.sw_batch_gather_plan.restype = i
     L.sw_score_batch_device.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(i),
                                         ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(i), i, ctypes.c_void_p, i,
                                         ctypes.c_void_p]
@@ -253,6 +255,13 @@ def batch_shard(npairs: int, ngpus: int, rank: int) -> tuple:
     lo, hi = ctypes.c_int(), ctypes.c_int()
     _check(lib().sw_batch_shard(npairs, ngpus, rank, ctypes.byref(lo), ctypes.byref(hi)))
     return lo.value, hi.value
+
+
+def batch_gather_plan(npairs: int, ngpus: int) -> list:
+    """[(count, offset)] per device of sw_score_batch_multi's RCCL gather to device 0 (no GPU call)."""
+    cnt, off = (ctypes.c_int * max(ngpus, 1))(), (ctypes.c_int * max(ngpus, 1))()
+    _check(lib().sw_batch_gather_plan(npairs, ngpus, cnt, off))
+    return [(cnt[r], off[r]) for r in range(ngpus)]
 
 
 def score_batch_device(d_arena_ptr: int, a_off, alen, b_off, blen, d_scores_ptr: int, flags: int = 0,

@@ -65,7 +65,7 @@ Params g_params;
 std::atomic<long long> g_opt_W{0}, g_opt_C{0}, g_opt_bytes{0}, g_opt_timeout{30}, g_opt_blocks{0}, g_opt_orient{0},
     g_opt_mode{-1}, g_opt_trace{0}, g_opt_duo_f16{1}, g_opt_f2stream{0}, g_opt_ring{-1}, g_opt_ring_rows{4096}, g_opt_f2_wgs{0}, g_opt_f2w{0}, g_opt_f2pwg{-1},
     g_opt_linear{-1}, g_opt_f3{1}, g_opt_slab_plain{0}, g_opt_duo_lds{1}, g_opt_duo_tab{1}, g_opt_duo_roles{1}, g_opt_f3hl{1},
-    g_opt_f3rhl{0};
+    g_opt_f3rhl{0}, g_opt_f3a{1};
 
 // Longest sequence the engine takes: granule buffers of m rows keep m * 16 in the
 // 32-bit record count of a buffer resource (sw_device.h linear_edge).
@@ -449,6 +449,15 @@ int finalize_mode(Job& job, const Params& prm, int cus) {
     if (job.mode == MODE_FLOW2 || (g_opt_mode.load() < 0 && job.mode == MODE_CHAIN)) {
         if (flow2_fits(job, prm)) {
             plan_flow2(job, flow2_w2_wanted(job, prm));
+            // the affine step in ring mode runs flow3's two-column affine kernel (sw_flow3ra_kernel:
+            // ring mode is throughput-bound, and two columns per lane issue 9 VALU per 64 cells
+            // against 10.5 at one): re-plan with two-column strips when they still take ring mode
+            if (job.ring && !job.f2w2 && !job.slab && g_opt_f3a.load() != 0 && g_opt_f2w.load() != 1 &&
+                (g_opt_C.load() == 0 || g_opt_C.load() == 64)) {
+                Job w2 = job;
+                plan_flow2(w2, true);
+                if (w2.ring) job = w2;
+            }
             job.f2_stream = job.ring || !flow2_staged(job, max_m);   // ring mode runs with streamed codes
             // ring mode (one pair of many groups per CU, C5): throughput-bound, so 64-row chunks
             // (half the per-chunk work per step) beat the shorter hand-off lag of 32 (C5 249 -> 220 ms)
@@ -667,6 +676,15 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
     const bool f3_base = g_opt_f3.load() != 0 && job.mode == MODE_FLOW2 && job.f2w2 && f2_lin && !job.pwg;
     const bool use_f3 = f3_base && ((!f2s && !job.ring && flow3_fits(max_m_f3, job.C)) ||
                                     (job.ring && edge == nullptr && (job.C == 64 || job.C == 32)));
+    // the general affine step (G_INIT != G_EXT, or option linear = 0) on flow3's staged kernel:
+    // one column per lane, rows in LDS, linear edges (C2 with affine constants); option f3a = 0
+    // keeps flow2
+    const bool use_f3a = g_opt_f3a.load() != 0 && job.mode == MODE_FLOW2 && !job.f2w2 && !f2_lin && !job.pwg &&
+                         !f2s && !job.ring && edge == nullptr && (job.C == 32 || job.C == 16) &&
+                         flow3_fits(max_m_f3, job.C, true);
+    // ... and in ring mode at two columns per lane (finalize_mode planned the strips for it)
+    const bool use_f3ra = g_opt_f3a.load() != 0 && job.mode == MODE_FLOW2 && job.f2w2 && !f2_lin && !job.pwg &&
+                          job.ring && edge == nullptr && job.C == 64;
     // duo batches at C = 64: strip hand-offs in LDS when the wrap buffer (a round's rows of
     // both pairs) fits the default dynamic-LDS limit; no boundary buffers in HBM then
     // and, at 4 or 8 columns per lane, the row codes from an LDS table when both fit two workgroups per CU
@@ -700,10 +718,11 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
         probe.f2_lin = f2_lin;
         probe.f2_w2 = job.f2w2;
         probe.f3_hl = use_f3 && job.C == 64 && g_opt_f3rhl.load() != 0;
+        probe.f3ra = use_f3ra;
         int fit = 0;
         for (;; --f2_wgs) {
             probe.f2_wgs = f2_wgs;
-            fit = use_f3 ? flow3_ring_resident(probe) : flow2_stream_resident(probe, true, edge != nullptr);
+            fit = use_f3 || use_f3ra ? flow3_ring_resident(probe) : flow2_stream_resident(probe, true, edge != nullptr);
             if (fit >= f2_wgs || f2_wgs == 1) break;
         }
         if (fit < 1) {
@@ -772,14 +791,17 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
     cfg.f3 = use_f3;
     cfg.f3_hl = use_f3 && ((!job.ring && job.C == 32 && g_opt_f3hl.load() != 0) ||
                            (job.ring && job.C == 64 && g_opt_f3rhl.load() != 0));
+    cfg.f3a = use_f3a;
+    cfg.f3ra = use_f3ra;
+    if (use_f3a) cfg.f3_hl = job.C == 32 && g_opt_f3hl.load() != 0;
     cfg.duo_wrap = duo_wrap;
     cfg.duo_tab = duo_tab;
     if (cfg.f2_w2 && job.C == 16 && !use_f3) {
         set_err("flow2: two columns per lane at C = 16 runs on flow3 only (rows staged in LDS, one GPU)");
         return -1;
     }
-    if (cfg.f2_w2 && !f2_lin) {   // the strips were cut for two columns per lane
-        set_err("flow2: two columns per lane needs the linear-gap step");
+    if (cfg.f2_w2 && !f2_lin && !use_f3ra) {   // the strips were cut for two columns per lane
+        set_err("flow2: two columns per lane needs the linear-gap step (or flow3's affine ring kernel)");
         return -1;
     }
     const int wpc = waves_per_cu(c, cfg);
@@ -811,9 +833,10 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
     kp.total_items = items;
     // epochs are never 0 (tag of a zeroed granule), nor one that makes flow3's granule key
     // k = epoch ^ 0x5BD1E995 zero in its low 5 bits: a zeroed 8-B granule passes its check when
-    // its second word equals k (staged) or k ^ (position << 5) (ring edges), which needs exactly that
+    // its second word equals k (staged) or k ^ (position << 5) (ring edges), which needs exactly that;
+    // the affine granules' E half is keyed k ^ 0x9E3779B9, held to the same rule
     do ++c->epoch;
-    while (c->epoch == 0 || ((c->epoch ^ 0x5BD1E995u) & 31u) == 0);
+    while (c->epoch == 0 || ((c->epoch ^ 0x5BD1E995u) & 31u) == 0 || ((c->epoch ^ 0x5BD1E995u ^ 0x9E3779B9u) & 31u) == 0);
     kp.epoch = c->epoch;
     kp.match = prm.match;
     kp.mismatch = prm.mismatch;
@@ -853,7 +876,7 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
     }
 
     if (time_kernel) HIPCHK(hipEventRecord(c->ev0, s));
-    HIPCHK(cfg.f3 ? launch_sw_flow3(cfg, kp, s)
+    HIPCHK(cfg.f3 || cfg.f3a || cfg.f3ra ? launch_sw_flow3(cfg, kp, s)
            : job.mode == MODE_FLOW2 ? launch_sw_flow2(cfg, kp, s) : launch_sw_strip(cfg, kp, s));
     if (time_kernel) HIPCHK(hipEventRecord(c->ev1, s));
 
@@ -868,7 +891,7 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
     t_stats.mode = job.mode;
     t_stats.variant = (cfg.duo_f16 ? 1 : 0) | (cfg.f2_stream ? 2 : 0) | (job.ring ? 4 : 0) | (cfg.f2_lin ? 8 : 0) |
                       (cfg.f2_w2 ? 16 : 0) | (cfg.f2_pwg ? 32 : 0) | (cfg.f3 ? 64 : 0) | (cfg.duo_wrap > 0 ? 128 : 0) |
-                      (cfg.duo_tab > 0 ? 256 : 0) | (cfg.f3_hl ? 512 : 0);
+                      (cfg.duo_tab > 0 ? 256 : 0) | (cfg.f3_hl ? 512 : 0) | (cfg.f3a || cfg.f3ra ? 1024 : 0);
     t_stats.boundary_bytes = (long long)(job.bnd_granules * sizeof(Granule));
     c->last = s;
     return 0;
@@ -1147,11 +1170,44 @@ MultiState& multi_state() {
     return *st;
 }
 
+// The gather of a multi-GPU batch: device r's shard [lo_r, hi_r) of the
+// int32 scores lands in device 0's gather buffer at offset lo_r.  Entry r of the plan: the
+// count device r sends and the offset it lands at (r = 0: the local device-to-device copy).
+// Host-only, so the send/recv plan is testable without a second GPU (sw_batch_gather_plan).
+void gather_plan(int npairs, int ngpus, int* count, int* offset) {
+    for (int r = 0; r < ngpus; ++r) {
+        int lo = 0, hi = 0;
+        batch_shard(npairs, ngpus, r, &lo, &hi);
+        count[r] = hi - lo;
+        offset[r] = lo;
+    }
+}
+
+// Restores the calling thread's HIP device on every exit path of score_multi.
+struct DeviceGuard {
+    int dev = -1;
+    ~DeviceGuard() {
+        if (dev >= 0) (void)hipSetDevice(dev);
+    }
+};
+
 #define NCCLCHK(expr)                                                                   \
     do {                                                                                \
         ncclResult_t r_ = (expr);                                                       \
         if (r_ != ncclSuccess) {                                                        \
             set_err("%s failed: %s", #expr, st.rccl.err ? st.rccl.err(r_) : "rccl");   \
+            return -1;                                                                  \
+        }                                                                               \
+    } while (0)
+
+// Inside ncclGroupStart/End: on a failed send or recv the group is closed before returning,
+// so the thread's RCCL group state is clean for the next call.
+#define NCCLCHK_GROUP(expr)                                                             \
+    do {                                                                                \
+        ncclResult_t r_ = (expr);                                                       \
+        if (r_ != ncclSuccess) {                                                        \
+            set_err("%s failed: %s", #expr, st.rccl.err ? st.rccl.err(r_) : "rccl");   \
+            (void)st.rccl.group_end();                                                  \
             return -1;                                                                  \
         }                                                                               \
     } while (0)
@@ -1181,19 +1237,19 @@ int score_multi(const HostPair* in, int npairs, const Params& prm, int* out, int
         st.workers.back()->start();
     }
     // every device scores its contiguous shard on its own host thread and stream
-    std::vector<int> rc(ngpus, 0), lo(ngpus), hi(ngpus);
+    std::vector<int> rc(ngpus, 0), cnt(ngpus), off(ngpus);
+    gather_plan(npairs, ngpus, cnt.data(), off.data());
     std::vector<int*> dptr(ngpus, nullptr);
     std::vector<float> kms(ngpus, 0.f);
     std::vector<std::string> errs(ngpus);
     for (int r = 0; r < ngpus; ++r) {
-        batch_shard(npairs, ngpus, r, &lo[r], &hi[r]);
         st.workers[r]->post([&, r] {
             if (hipSetDevice(r) != hipSuccess) {
                 rc[r] = -1;
                 errs[r] = "hipSetDevice failed";
                 return;
             }
-            rc[r] = score_host_device(in + lo[r], hi[r] - lo[r], prm, &dptr[r], &kms[r]);
+            rc[r] = score_host_device(in + off[r], cnt[r], prm, &dptr[r], &kms[r]);
             if (rc[r]) errs[r] = t_err;
         });
     }
@@ -1203,8 +1259,8 @@ int score_multi(const HostPair* in, int npairs, const Params& prm, int* out, int
             set_err("sw_score_batch_multi: device %d: %s", r, errs[r].c_str());
             return -1;
         }
-    int dev0 = 0;
-    HIPCHK(hipGetDevice(&dev0));
+    DeviceGuard dg;
+    HIPCHK(hipGetDevice(&dg.dev));
     while ((int)st.streams.size() < ngpus) {
         HIPCHK(hipSetDevice((int)st.streams.size()));
         hipStream_t sx = nullptr;
@@ -1213,18 +1269,24 @@ int score_multi(const HostPair* in, int npairs, const Params& prm, int* out, int
     }
     HIPCHK(hipSetDevice(0));
     if ((size_t)npairs > st.gather_cap) {
-        if (st.d_gather) HIPCHK(hipFree(st.d_gather));
-        if (st.h_scores) HIPCHK(hipHostFree(st.h_scores));
-        st.d_gather = nullptr;
-        st.h_scores = nullptr;
-        st.gather_cap = 0;
-        HIPCHK(hipMalloc((void**)&st.d_gather, (size_t)npairs * sizeof(int)));
-        HIPCHK(hipHostMalloc((void**)&st.h_scores, (size_t)npairs * sizeof(int), hipHostMallocDefault));
+        // allocate the new buffers first, commit them only when both exist
+        int* dg_new = nullptr;
+        int* hs_new = nullptr;
+        HIPCHK(hipMalloc((void**)&dg_new, (size_t)npairs * sizeof(int)));
+        if (hipHostMalloc((void**)&hs_new, (size_t)npairs * sizeof(int), hipHostMallocDefault) != hipSuccess) {
+            (void)hipFree(dg_new);
+            set_err("sw_score_batch_multi: hipHostMalloc of %d scores failed", npairs);
+            return -1;
+        }
+        if (st.d_gather) (void)hipFree(st.d_gather);
+        if (st.h_scores) (void)hipHostFree(st.h_scores);
+        st.d_gather = dg_new;
+        st.h_scores = hs_new;
         st.gather_cap = (size_t)npairs;
     }
     // device 0's own shard, then the others' int32 scores over RCCL (the only exchange)
-    if (hi[0] > lo[0])
-        HIPCHK(hipMemcpyAsync(st.d_gather, dptr[0], (size_t)(hi[0] - lo[0]) * sizeof(int), hipMemcpyDeviceToDevice,
+    if (cnt[0] > 0)
+        HIPCHK(hipMemcpyAsync(st.d_gather + off[0], dptr[0], (size_t)cnt[0] * sizeof(int), hipMemcpyDeviceToDevice,
                               st.streams[0]));
     if (ngpus > 1) {
         auto it = st.comms.find(ngpus);
@@ -1238,10 +1300,9 @@ int score_multi(const HostPair* in, int npairs, const Params& prm, int* out, int
         const std::vector<ncclComm_t>& cl = it->second;
         NCCLCHK(st.rccl.group_start());
         for (int r = 1; r < ngpus; ++r) {
-            const size_t cnt = (size_t)(hi[r] - lo[r]);
-            if (!cnt) continue;
-            NCCLCHK(st.rccl.send(dptr[r], cnt, ncclInt32, 0, cl[r], st.streams[r]));
-            NCCLCHK(st.rccl.recv(st.d_gather + lo[r], cnt, ncclInt32, r, cl[0], st.streams[0]));
+            if (!cnt[r]) continue;
+            NCCLCHK_GROUP(st.rccl.send(dptr[r], (size_t)cnt[r], ncclInt32, 0, cl[r], st.streams[r]));
+            NCCLCHK_GROUP(st.rccl.recv(st.d_gather + off[r], (size_t)cnt[r], ncclInt32, r, cl[0], st.streams[0]));
         }
         NCCLCHK(st.rccl.group_end());
     }
@@ -1252,7 +1313,6 @@ int score_multi(const HostPair* in, int npairs, const Params& prm, int* out, int
         HIPCHK(hipSetDevice(r));
         HIPCHK(hipStreamSynchronize(st.streams[r]));
     }
-    HIPCHK(hipSetDevice(dev0));
     std::memcpy(out, st.h_scores, (size_t)npairs * sizeof(int));
     t_stats = sw_stats{};
     for (int r = 0; r < ngpus; ++r) t_stats.kernel_ms = std::max(t_stats.kernel_ms, kms[r]);
@@ -1261,6 +1321,7 @@ int score_multi(const HostPair* in, int npairs, const Params& prm, int* out, int
     return 0;
 }
 #undef NCCLCHK
+#undef NCCLCHK_GROUP
 
 hipError_t raise_dyn_lds(const void* fn, int bytes) {
     static std::mutex mu;
@@ -1357,6 +1418,15 @@ int sw_batch_shard(int npairs, int ngpus, int rank, int* lo, int* hi) {
         return -1;
     }
     batch_shard(npairs, ngpus, rank, lo, hi);
+    return 0;
+}
+
+int sw_batch_gather_plan(int npairs, int ngpus, int* count, int* offset) {
+    if (npairs < 0 || ngpus < 1 || !count || !offset) {
+        set_err("sw_batch_gather_plan: invalid arguments");
+        return -1;
+    }
+    gather_plan(npairs, ngpus, count, offset);
     return 0;
 }
 
@@ -1647,6 +1717,9 @@ int sw_set_option(const char* key, long long v) {
     } else if (k == "f3rhl") {   // 1: flow3 ring launches at C = 64 with half-chunk in-workgroup links
         if (v < 0 || v > 1) return -1;
         g_opt_f3rhl = v;
+    } else if (k == "f3a") {   // 1 (default): staged affine-step launches on flow3 (sw_flow3a_kernel), 0: flow2
+        if (v < 0 || v > 1) return -1;
+        g_opt_f3a = v;
     } else if (k == "duo_roles") {   // 1 (default): duo strip roles complementary per SIMD across a CU's workgroups
         if (v < 0 || v > 1) return -1;
         g_opt_duo_roles = v;
@@ -1696,6 +1769,7 @@ long long sw_get_option(const char* key) {
     if (k == "duo_roles") return g_opt_duo_roles;
     if (k == "f3hl") return g_opt_f3hl;
     if (k == "f3rhl") return g_opt_f3rhl;
+    if (k == "f3a") return g_opt_f3a;
     return -1;
 }
 

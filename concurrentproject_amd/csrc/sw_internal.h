@@ -135,6 +135,8 @@ struct LaunchCfg {
     bool f2_pwg = false;    // MODE_FLOW2 batch: a pair per workgroup, all hand-offs in LDS (C = 64, streamed)
     bool f3 = false;        // MODE_FLOW2 staged two-column linear-gap launch on the flow3 kernel (sw_flow3.hip)
     bool f3_hl = false;     // flow3 staged at C = 32: in-workgroup links hand off every half chunk
+    bool f3a = false;       // MODE_FLOW2 staged one-column launch with the affine step on flow3 (sw_flow3a_kernel)
+    bool f3ra = false;      // MODE_FLOW2 ring-mode two-column launch with the affine step on flow3 (sw_flow3ra_kernel)
     int duo_wrap = 0;       // MODE_DUO at C = 64: > 0 = strip hand-offs in LDS (sw_duo_lds_kernel), this many
                             // wrap-buffer slots (a power of two >= every m_pad); 0 = HBM granules
     int duo_tab = 0;        // with duo_wrap, W % 4 == 0: > 0 = row codes from an LDS table of this many words
@@ -205,7 +207,7 @@ hipError_t raise_dyn_lds(const void* fn, int bytes);
 hipError_t launch_sw_flow2(const LaunchCfg& cfg, const KParams& kp, hipStream_t stream);
 // flow3 (sw_flow3.hip): flow2's staged W2 linear-gap kernel with hand-scheduled chunk loops
 hipError_t launch_sw_flow3(const LaunchCfg& cfg, const KParams& kp, hipStream_t stream);
-bool flow3_fits(int max_m, int C);
+bool flow3_fits(int max_m, int C, bool aff = false);
 // workgroups per CU resident for a flow3 ring-mode launch (its LDS pad of cfg.f2_wgs), -1 on error
 int flow3_ring_resident(const LaunchCfg& cfg);
 int flow2_waves_per_cu(int C);

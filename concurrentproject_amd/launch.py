@@ -97,13 +97,21 @@ def gpu_count(environ=None, root: Optional[str] = None, dri: Optional[str] = Non
     gpus = kfd_gpus(root, dri)
     rocr = env.get("ROCR_VISIBLE_DEVICES")
     if rocr is not None:
-        ids = {"GPU-%x" % int(g.get("unique_id", "0")): g for g in gpus}
+        # UUID tokens: ROCr prints GPU- and 16 zero-padded hex digits; compare the numbers
+        ids = {int(g.get("unique_id", "0")): g for g in gpus}
         keep = []
         for tok in [t.strip() for t in rocr.split(",") if t.strip()]:
             if tok.isdigit() and int(tok) < len(gpus):
                 keep.append(gpus[int(tok)])
-            elif tok.lower() in {k.lower() for k in ids}:
-                keep.append(next(v for k, v in ids.items() if k.lower() == tok.lower()))
+                continue
+            uid = None
+            if tok[:4].upper() == "GPU-":
+                try:
+                    uid = int(tok[4:], 16)
+                except ValueError:
+                    uid = None
+            if uid is not None and uid in ids:
+                keep.append(ids[uid])
             else:
                 break
         gpus = keep

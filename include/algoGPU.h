@@ -75,12 +75,22 @@ int sw_score_batch(const unsigned char* const* a, const int* alen,
  * one group; RCCL is loaded at the first call with ngpus > 1) -- the only exchange, no
  * data-path collective.  Synchronous like the reference ABI; scores_out in pair order.
  * Returns 0, or -1 with sw_last_error() (e.g. ngpus above the visible devices).
- * Callers: the reference harness's batched loops (TestFileWithGPU.cpp:82-94). */
+ * Callers: the reference harness's batched loops (TestFileWithGPU.cpp:82-94).
+ * UNVERIFIED ON HARDWARE for ngpus > 1: the build's GPU boxes have one GPU, so the RCCL
+ * branch has only run through its host-side plan (sw_batch_gather_plan, CPU-tested).
+ * Lifetime: the first call starts one host worker thread per device used; the threads are
+ * detached and live for the rest of the process (never joined), as do their engine contexts,
+ * streams and the RCCL communicators. */
 int sw_score_batch_multi(const unsigned char* const* a, const int* alen,
                          const unsigned char* const* b, const int* blen,
                          int npairs, int* scores_out, int ngpus);
 /* Shard [*lo, *hi) of rank `rank` of ngpus for npairs pairs (no GPU call).  0 or -1. */
 int sw_batch_shard(int npairs, int ngpus, int rank, int* lo, int* hi);
+/* The gather sw_score_batch_multi runs (no GPU call): count[r] scores of device r land in
+ * device 0's gather buffer at offset[r] (r = 0: the local copy; r > 0: one ncclSend from
+ * device r matched by one ncclRecv on device 0, skipped when count[r] == 0).  count and
+ * offset hold ngpus ints.  0 or -1. */
+int sw_batch_gather_plan(int npairs, int ngpus, int* count, int* offset);
 
 /* Batch whose sequences are already resident in device memory (one arena,
  * byte offsets per sequence).  Offsets/lengths are HOST arrays; d_scores is a

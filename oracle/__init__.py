@@ -175,6 +175,33 @@ def score_batch(pairs, params: Params = DEFAULT, threads: int = 8, full: bool = 
     return list(out)
 
 
+def similar_pair(seed: int, n: int) -> tuple:
+    """A pair with long alignments and long gaps (numpy PCG64, so any machine makes the same
+    bytes): b is a copy of random DNA a with 8 % substitutions and an indel of 1..n/256 bases
+    every ~n/64 positions, so G_INIT != G_EXT scores run through long E and F legs at any size
+    (the generator's uniform pairs score tiny alignments with affine constants)."""
+    rng = np.random.default_rng(seed)
+    acgt = np.frombuffer(b"ACGT", np.uint8)
+    a = acgt[rng.integers(0, 4, n)]
+    b = a.copy()
+    mut = rng.random(n) < 0.08
+    b[mut] = acgt[rng.integers(0, 4, int(mut.sum()))]
+    cuts = np.sort(rng.integers(0, n, 64))
+    parts, prev = [], 0
+    for c in cuts:
+        parts.append(b[prev:c])
+        ln = int(rng.integers(1, max(2, n // 256)))
+        if rng.random() < 0.5:
+            prev = min(n, c + ln)                            # deletion
+        else:
+            parts.append(acgt[rng.integers(0, 4, ln)])       # insertion
+            prev = c
+    parts.append(b[prev:])
+    b = np.concatenate(parts)
+    b = np.resize(b, n) if len(b) < n else b[:n]
+    return np.ascontiguousarray(a), np.ascontiguousarray(b)
+
+
 def gen_pair(seed: int, length: int) -> tuple:
     """cudaSmithM.cu:200-212 generator: mt19937_64(seed), a[i] then b[i]."""
     a = np.empty(length, dtype=np.uint8); b = np.empty(length, dtype=np.uint8)

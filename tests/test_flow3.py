@@ -94,15 +94,16 @@ def test_flow3_matches_flow2(engine):
 
 
 def test_flow3_only_where_it_applies(engine, oracle_mod):
-    """The affine step (G_INIT != G_EXT, or linear = 0) and C = 64 stay on flow2."""
+    """The affine step (G_INIT != G_EXT, or linear = 0) runs flow3's affine kernel (variant bit
+    1024, test_flow3_affine.py), not the two-column one; C = 64 stays on flow2."""
     rng = np.random.default_rng(33)
     a, b = _pairs(rng, [(2017, 2100)])[0]
     prm = engine.Params(2, -3, 5, 2)
     assert engine.score(a, b, prm) == oracle_mod.score_linear(a, b, oracle_mod.Params(2, -3, 5, 2))
-    assert not engine.last_stats()["variant"] & 64
+    assert not engine.last_stats()["variant"] & 64 and engine.last_stats()["variant"] & 1024
     engine.set_option("linear", 0)
     assert engine.score(a, b) == oracle_mod.score_linear(a, b)
-    assert not engine.last_stats()["variant"] & 64
+    assert not engine.last_stats()["variant"] & 64 and engine.last_stats()["variant"] & 1024
     engine.set_option("linear", -1)
     engine.set_option("C", 64)
     engine.set_option("mode", 5)

@@ -125,6 +125,10 @@ def test_gpu_count_from_kfd_topology(tmp_path):
     assert gpu_count({"HIP_VISIBLE_DEVICES": ""}, topo, dri) == 0
     assert gpu_count({"ROCR_VISIBLE_DEVICES": "2,3", "HIP_VISIBLE_DEVICES": "1"}, topo, dri) == 1
     assert gpu_count({"ROCR_VISIBLE_DEVICES": "GPU-%x" % 1003}, topo, dri) == 1
+    # ROCr's own form: GPU- and 16 zero-padded hex digits (any case)
+    assert gpu_count({"ROCR_VISIBLE_DEVICES": "GPU-%016x" % 1003}, topo, dri) == 1
+    assert gpu_count({"ROCR_VISIBLE_DEVICES": "gpu-%016X,GPU-%016x" % (1003, 1004)}, topo, dri) == 2
+    assert gpu_count({"ROCR_VISIBLE_DEVICES": "GPU-%016x,GPU-zz" % 1003}, topo, dri) == 1   # stops at a bad token
     with pytest.raises(LaunchError, match="cannot count GPUs"):
         gpu_count({}, str(tmp_path / "missing"), dri)
 

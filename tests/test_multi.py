@@ -21,6 +21,24 @@ def test_shard_plan_matches_dist(npairs, ngpus):
     assert all(a[1] == b[0] for a, b in zip(got, got[1:]))
 
 
+@pytest.mark.parametrize("npairs", [0, 1, 3, 7, 1024, 8191, 8192, 8193])
+@pytest.mark.parametrize("ngpus", [1, 2, 3, 8])
+def test_gather_plan(npairs, ngpus):
+    """The RCCL gather of sw_score_batch_multi (the only exchange): device r sends exactly its
+    shard's scores, which land at the shard's start in device 0's buffer, so the gathered vector
+    is every score once, in pair order -- checked without a second GPU."""
+    plan = sw.batch_gather_plan(npairs, ngpus)
+    assert plan == [(hi - lo, lo) for lo, hi in (shard_bounds(npairs, ngpus, r) for r in range(ngpus))]
+    covered = [0] * npairs
+    for cnt, off in plan:
+        assert cnt >= 0 and 0 <= off and off + cnt <= npairs
+        for k in range(off, off + cnt):
+            covered[k] += 1
+    assert covered == [1] * npairs
+    with pytest.raises(sw.SwError, match="invalid"):
+        sw.batch_gather_plan(10, 0)
+
+
 def test_shard_plan_rejects_bad_arguments():
     for args in ((10, 0, 0), (10, 2, 2), (-1, 2, 0), (10, 2, -1)):
         with pytest.raises(sw.SwError, match="invalid"):

@@ -692,16 +692,613 @@ def emit_ring():
 
 OUT_RING = os.path.join(ROOT, "concurrentproject_amd", "csrc", "sw_flow3r_loops.inc")
 
+# ============================================================================================
+# The general affine (Gotoh) step, staged organisation (C2 with G_INIT != G_EXT):
+# sw_flow3.hip sw_flow3a_kernel, sw_flow3a_loops.inc.  ONE column per lane (63 new columns
+# per strip): a single long pair is latency-bound, and the critical path is (m + n / W) steps
+# of (ops per step) instructions of a lone wave, 10.5 VALU at W = 1 against 18 at W = 2,
+# so W = 1 is the shorter path for this step.  Two quantities flow
+# lane to lane (H - G_INIT and E - G_EXT), each through a tied DPP-add and a rotating I/O
+# register; LDS links carry both as one 8-B slot, workgroup edges as 16-B granules
+# {H - GI, (H - GI) ^ ek, E - GE, (E - GE) ^ ek2} whose two halves each carry their own tag.
+# Step (lane l, row i = k - l; main.cpp:54-66, clamped as DESIGN.md section 2):
+#   t   = L0H + s(q, d) + G_INIT        SDWA byte of the 4-row profile perm; L0H = last hgL
+#   L0H = wave_shl1(IOH), L0E = wave_shl1(IOE)    rotation; lane 63 keeps last (hgL, ehL)
+#   hgL = IOH = H[l-1] - G_INIT, ehL = IOE = E[l-1] - G_EXT   tied DPP-adds (lane 0: inflow)
+#   F   = max3(fh, hgO, 0)              fh = F(i-1) - G_EXT, hgO = H(i-1) - G_INIT
+#   E   = max(ehL, hgL)                 (>= -G_INIT; H sees it through max3 with F >= 0)
+#   H   = max3(t, E, F);  fh = F - G_EXT;  hgO = H - G_INIT;  M = max3(M, t, t') every 2 steps
+# Registers: v64..v67 IO/L0 (even step: IOH v64, IOE v65, L0H v66, L0E v67; odd: swapped
+# pairwise, so the chunk top always finds the I/O pair in v[64:65]), v68 H, v69 hgO, v70 F,
+# v71 fh, v72 E, v73/v74 t of even/odd steps, v75 score bytes of 4 rows, v76 M,
+# v[80:87] / v[88:95] row codes of the even / odd chunk, v[96:97] inflow row, v98 producer
+# word read, v99 code address, v100 inflow address, v101 outflow address, v102 producer word
+# value, v103 consumer word value, v104 back-pressure read, v105 mid-publish address,
+# v[106:107] mid-chunk inflow row, v[108:111] granule, v112 granule offset (row * 16),
+# v113 masked offset; SGPRs as gen_role.
+# ============================================================================================
+SZA = 8                  # bytes per LDS ring slot: (H - G_INIT, E - G_EXT)
+
+
+def step_aff1(a, b, even):
+    """One anti-diagonal step of the one-column affine step (10.5 VALU, 64 cells)."""
+    ioh, ioe, l0h, l0e = ("v64", "v65", "v66", "v67") if even else ("v66", "v67", "v64", "v65")
+    t = "v73" if even else "v74"
+    a(f"v_add_u32_sdwa {t}, sext(v75), {l0h} dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_{b} src1_sel:DWORD")
+    a(f"v_mov_b32_dpp {l0h}, {ioh} wave_shl:1 row_mask:0xf bank_mask:0xf")
+    a(f"v_add_u32_dpp {ioh}, v68, %[ng] wave_shr:1 row_mask:0xf bank_mask:0xf")
+    a(f"v_mov_b32_dpp {l0e}, {ioe} wave_shl:1 row_mask:0xf bank_mask:0xf")
+    a(f"v_add_u32_dpp {ioe}, v72, %[nge] wave_shr:1 row_mask:0xf bank_mask:0xf")
+    a("v_max3_i32 v70, v71, v69, 0")
+    a(f"v_max_i32 v72, {ioe}, {ioh}")
+    a(f"v_max3_i32 v68, {t}, v72, v70")
+    a("v_subrev_u32 v71, %[GE], v70")
+    a("v_subrev_u32 v69, %[GI], v68")
+    if not even:
+        a("v_max3_i32 v76, v76, v73, v74")
+
+
+def granule_aff(a, rows):
+    """Publish the `rows` newest outflow rows (lanes 64-rows..63 of the I/O pair v[64:65], mask
+    %[m48]) as 16-B granules {H-GI, (H-GI) ^ ek, E-GE, (E-GE) ^ ek2} at row * 16, write-through."""
+    a("v_mov_b32 v108, v64")
+    a("v_xor_b32 v109, %[ek], v64")
+    a("v_mov_b32 v110, v65")
+    a("v_xor_b32 v111, %[ek2], v65")
+    a("v_cndmask_b32_e64 v113, -16, v112, %[m48]")
+    a(f"v_add_u32 v112, {rows * 16:#x}, v112")
+    a("buffer_store_dwordx4 v[108:111], v113, %[rsrc], 0 offen sc1")
+
+
+def book_aff(a, p, lds_in, lds_out, C, H):
+    a(f"s_add_i32 s40, s40, {C}")
+    a(f"s_add_u32 s41, s41, {SZA * C:#x}")
+    a(f"s_and_b32 s41, s41, {(R - 1) * SZA:#x}")
+    if lds_out:
+        a("v_add_u32 v101, s41, %[lout]")
+        a(f"v_add_u32 v102, {C if H == C else C - H}, v102")
+    if lds_in:
+        a("v_add_u32 v100, s41, %[lin]")
+        a(f"v_add_u32 v103, {C}, v103")
+    if p == 1:
+        a(f"v_add_u32 v99, {2 * C}, v99")
+
+
+def gen_role_aff(IN, OUT_, C=32, hl=True):
+    """gen_role's staged loop (same chunks, words, half-chunk links, speculative inflow read
+    4 steps ahead, granules every half chunk) around the one-column affine step."""
+    L = []
+    a = L.append
+    lds_in, lds_out, gran = IN == "lds", OUT_ == "lds", OUT_ == "gran"
+    H = C // 2 if hl else C
+    ng = C // 4
+    ncr = ng // 4                       # 16-B code reads per chunk
+    nw = 2 if lds_out else 0
+    assert C in (16, 32) and (not hl or C == 32)
+    a("s_nop 4")
+    a("s_waitcnt vmcnt(0) lgkmcnt(0)")
+    for r in ("v68", "v70", "v72", "v76"):
+        a(f"v_mov_b32 {r}, 0")
+    a("v_mov_b32 v69, %[ng]")
+    a("v_mov_b32 v71, %[nge]")
+    a("v_mov_b32 v64, %[ng]")
+    a("v_mov_b32 v66, %[ng]")
+    a("v_mov_b32 v65, %[nge]")
+    a("v_mov_b32 v67, %[nge]")
+    a("v_mov_b32 v99, %[code]")
+    a("s_mov_b32 s40, 0")
+    a(f"s_movk_i32 s41, {(64 - C) * SZA:#x}")
+    a("s_mov_b32 s45, 0")
+    a("s_mov_b32 s46, 0")
+    a(f"s_movk_i32 s44, {R}")
+    if lds_out:
+        a(f"v_mov_b32 v102, {-64 - H}")
+        a("v_add_u32 v101, s41, %[lout]")
+    if lds_in:
+        a(f"v_mov_b32 v103, {R + H}")
+        a("v_add_u32 v100, s41, %[lin]")
+        if hl:
+            a("s_mov_b32 s50, 0xffff")
+            a("s_mov_b32 s51, 0")
+    if gran:
+        a("v_mov_b32 v112, %[lrow]")
+    for q in range(ncr):
+        a(f"ds_read_b128 v[{80 + 4 * q}:{83 + 4 * q}], v99 offset:{16 * q}")
+    if lds_in:
+        a("ds_read_b32 v98, %[pin]")
+        a("ds_read_b64 v[96:97], v100")
+    a("L_loop_%=:")
+    for p in (0, 1):
+        cur = 80 if p == 0 else 88
+        nxt = 88 if p == 0 else 80
+        obase = C if p == 0 else 2 * C
+        if lds_out:
+            if p == 0:
+                if hl:
+                    a(f"s_add_u32 s52, s40, {H}")
+                    a("s_cmp_lt_i32 s44, s52")
+                else:
+                    a("s_cmp_lt_i32 s44, s40")
+                a(f"s_cbranch_scc1 L_bp{p}_%=")
+                a(f"L_bpr{p}_%=:")
+            a(f"ds_write2st64_b64 v101, v[64:65], v[64:65] offset1:{R * SZA // 512}")
+            a("ds_write_b32 %[pout], v102")
+        if gran:
+            granule_aff(a, C // 2)
+        for q in range(ncr):
+            a(f"ds_read_b128 v[{nxt + 4 * q}:{nxt + 4 * q + 3}], v99 offset:{obase + 16 * q}")
+        if lds_in:
+            after = 1 + nw + ncr
+            a(f"s_waitcnt lgkmcnt({after})")
+            a("v_readfirstlane_b32 s43, v98")
+            a("s_cmp_lt_i32 s43, s40")
+            a(f"s_cbranch_scc1 L_in{p}_%=")
+            a(f"L_inr{p}_%=:")
+            a(f"s_waitcnt lgkmcnt({after - 1})")
+            a("v_mov_b32 v64, v96")
+            a("v_mov_b32 v65, v97")
+            a("ds_write_b32 %[qme], v103")
+        else:
+            a(f"s_waitcnt lgkmcnt({nw + ncr})")
+            a("v_mov_b32 v64, %[ng]")
+            a("v_mov_b32 v65, %[nge]")
+        for u in range(ng):
+            if u == ng - 1:
+                book_aff(a, p, lds_in, lds_out, C, H)
+                if lds_in:
+                    a("ds_read_b32 v98, %[pin]")
+                    a("ds_read_b64 v[96:97], v100")
+            if hl and lds_in and u == ng // 2 - MID_AHEAD:
+                a("ds_read_b32 v98, %[pin]")
+                a(f"ds_read_b64 v[106:107], v100 offset:{SZA * H}")
+            if hl and u == ng // 2:
+                if lds_out:
+                    a("v_add_u32 v105, %[lmid], v101")
+                    a(f"v_add_u32 v102, {H}, v102")
+                    a(f"ds_write2st64_b64 v105, v[64:65], v[64:65] offset1:{R * SZA // 512}")
+                    a("ds_write_b32 %[pout], v102")
+                if lds_in:
+                    a(f"s_waitcnt lgkmcnt({1 + (2 if lds_out else 0)})")
+                    a("v_readfirstlane_b32 s43, v98")
+                    if not (lds_out and p == 0):
+                        a(f"s_add_u32 s52, s40, {H}")
+                    a("s_cmp_lt_i32 s43, s52")
+                    a(f"s_cbranch_scc1 L_mid{p}_%=")
+                    a(f"L_midr{p}_%=:")
+                    a(f"s_waitcnt lgkmcnt({2 if lds_out else 0})")
+                    a("v_cndmask_b32_e64 v64, v64, v106, s[50:51]")
+                    a("v_cndmask_b32_e64 v65, v65, v107, s[50:51]")
+            a(f"v_perm_b32 v75, %[pA], %[k80], v{cur + u}")
+            for b in range(4):
+                step_aff1(a, b, b % 2 == 0)
+            if gran and u == ng // 2 - 1:
+                granule_aff(a, C // 2)
+    a("s_cmp_lt_i32 s40, %[end]")
+    a("s_cbranch_scc1 L_loop_%=")
+    if lds_out:
+        a("s_cmp_lt_i32 s44, s40")
+        a("s_cbranch_scc1 L_bpx_%=")
+        a("L_bpxr_%=:")
+        a(f"ds_write2st64_b64 v101, v[64:65], v[64:65] offset1:{R * SZA // 512}")
+        a(f"v_mov_b32 v102, {BIG:#x}")
+        a("ds_write_b32 %[pout], v102")
+    if gran:
+        granule_aff(a, C // 2)
+    a("s_waitcnt vmcnt(0) lgkmcnt(0)")
+    a("v_mov_b32 %[M], v76")
+    a("s_mov_b32 %[fail], s45")
+    a("s_mov_b32 %[slow], s46")
+    a("s_branch L_done_%=")
+    if lds_in:
+        for p in (0, 1):
+            slow_wait(a, f"L_in{p}_%=", f"L_inr{p}_%=", "v98", "%[pin]", "s43", reread="ds_read_b64 v[96:97], v100")
+            if hl:
+                slow_wait(a, f"L_mid{p}_%=", f"L_midr{p}_%=", "v98", "%[pin]", "s43",
+                          reread=f"ds_read_b64 v[106:107], v100 offset:{SZA * H}", target="s52")
+    if lds_out:
+        slow_wait(a, "L_bp0_%=", "L_bpr0_%=", "v104", "%[qnx]", "s44", target="s52" if hl else "s40")
+        slow_wait(a, "L_bpx_%=", "L_bpxr_%=", "v104", "%[qnx]", "s44")
+    a("L_done_%=:")
+    return L
+
+
+CLOBBERS_AFF = ['"v%d"' % r for r in range(64, 114) if r not in (77, 78, 79)] + \
+    ['"s%d"' % r for r in range(40, 53) if r != 42 and r != 47] + ['"scc"', '"vcc"', '"memory"']
+OUT_AFF = os.path.join(ROOT, "concurrentproject_amd", "csrc", "sw_flow3a_loops.inc")
+
+
+def emit_aff():
+    out = ["// GENERATED by tools/gen_flow3.py -- do not edit.  The flow3 affine-step chunk loops",
+           "// (sw_flow3.hip sw_flow3a_kernel): one inline-asm block per (chunk rows C, half-chunk LDS links HL,",
+           "// strip role), R = %d ring rows of 8-B slots, inflow read 4 steps ahead, granules every half chunk." % R,
+           "// Operands: see F3ALoop in sw_flow3.hip; fixed registers: tools/gen_flow3.py (gen_role_aff).",
+           "#pragma once", ""]
+    for C, hl in ((32, 1), (32, 0), (16, 0)):
+        for IN in ROLES_IN:
+            for OUT_ in ROLES_OUT:
+                body = gen_role_aff(IN, OUT_, C, bool(hl))
+                out.append("template <> __device__ __forceinline__ F3Res f3a_loop<%d, %d, F3_%s, F3_%s>(const F3ALoop& x) {"
+                           % (C, hl, IN.upper(), OUT_.upper()))
+                out.append("    F3Res r;")
+                out.append("    asm volatile(")
+                for line in body:
+                    out.append('        "%s\\n\\t"' % line)
+                out.append('        : [M] "=v"(r.M), [fail] "=s"(r.fail), [slow] "=s"(r.slow)')
+                out.append('        : [pA] "v"(x.pA), [ng] "v"(x.ng), [nge] "v"(x.nge), [GI] "s"(x.GI), [GE] "s"(x.GE),')
+                out.append('          [k80] "s"(x.k80), [code] "v"(x.code), [lin] "v"(x.lin), [lout] "v"(x.lout),')
+                out.append('          [pin] "v"(x.pin), [pout] "v"(x.pout), [qme] "v"(x.qme), [qnx] "v"(x.qnx),')
+                out.append('          [end] "s"(x.end), [dlo] "s"(x.dlo), [dhi] "s"(x.dhi), [rsrc] "s"(x.rsrc),')
+                out.append('          [ek] "s"(x.ek), [ek2] "s"(x.ek2), [lrow] "v"(x.lrow), [m48] "s"(x.m48),')
+                out.append('          [lmid] "v"(x.lmid)')
+                out.append("        : " + ", ".join(CLOBBERS_AFF) + ");")
+                out.append("    return r;")
+                out.append("}")
+                out.append("")
+    return "\n".join(out)
+
+
+# ============================================================================================
+# The general affine step in ring mode (C5 with G_INIT != G_EXT): sw_flow3.hip
+# sw_flow3ra_kernel, sw_flow3ra_loops.inc.  Ring mode is throughput-bound (4 waves per SIMD),
+# where what counts is issue cost per cell: TWO columns per lane, 18 VALU for 128 cells
+# (13 slow-class) against 10.5 for 64 (8.5 slow) at one column.  gen_role_ring's organisation
+# at C = 64 (no half-chunk links) with two flows: LDS slots of 8 B (H - GI, E - GE) and ring
+# granules of 16 B {H-GI, (H-GI)^ek^(pos<<5), E-GE, (E-GE)^ek2^(pos<<5)}.
+# Step (lane l: columns A, B; main.cpp:54-66 clamped as DESIGN.md section 2):
+#   tA = L0H + s_A + G_INIT, tB = H_A(i-1) + s_B       (diagonals; profiles prof2 / prof3)
+#   L0H/L0E = wave_shl1(IOH/IOE); IOH = H_B[l-1] - GI, IOE = E_B[l-1] - GE   (lane 0: inflow)
+#   F_A = max3(fhA, hgOA, 0); E_A = max(IOE, IOH); H_A = max3(tA, E_A, F_A)
+#   fhA = F_A - GE; hgOA = H_A - GI; E_B = max(E_A - GE, hgOA)
+#   F_B = max3(fhB, hgOB, 0); H_B = max3(tB, E_B, F_B); fhB = F_B - GE; hgOB = H_B - GI
+#   M = max3(M, tA, tB)
+# Registers: v40..v43 IO/L0 (even step: IOH v40, IOE v41, L0H v42, L0E v43; odd swapped
+# pairwise), v44 H_A, v45 hgOA, v46 fhA, v47 H_B, v48 hgOB, v49 fhB, v50 E_B, v51 tA,
+# v52 tB, v53 F (temp), v54 E_A / E_A - GE (temp), v55 / v56 score bytes A / B, v57 M,
+# v[58:73] / v[74:89] row codes of the even / odd chunk, v[90:93] granule inflow (or the LDS
+# inflow row v[90:91]), v94 producer word read, v95 code read address, v96 / v97 LDS inflow /
+# outflow address, v98 / v99 producer / consumer word values, v100 back-pressure read, v101 raw
+# row byte, v102 row code, v103 code write address, v[104:107] granule outflow, v108 its slot
+# offset, v109 its masked offset, v110 its position << 5, v111 granule inflow offset, v112 its
+# position << 5, v113 scratch, v114 consumer report, v115 code read offset, v116 raw row,
+# v117 granule outflow row; SGPRs as gen_role_ring.
+# ============================================================================================
+
+
+def step_aff2(a, b, even):
+    """One anti-diagonal step of the two-column affine step (18 VALU, 128 cells)."""
+    ioh, ioe, l0h, l0e = ("v40", "v41", "v42", "v43") if even else ("v42", "v43", "v40", "v41")
+    a(f"v_add_u32_sdwa v51, sext(v55), {l0h} dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_{b} src1_sel:DWORD")
+    a(f"v_add_u32_sdwa v52, sext(v56), v44 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_{b} src1_sel:DWORD")
+    a(f"v_mov_b32_dpp {l0h}, {ioh} wave_shl:1 row_mask:0xf bank_mask:0xf")
+    a(f"v_add_u32_dpp {ioh}, v47, %[ng] wave_shr:1 row_mask:0xf bank_mask:0xf")
+    a(f"v_mov_b32_dpp {l0e}, {ioe} wave_shl:1 row_mask:0xf bank_mask:0xf")
+    a(f"v_add_u32_dpp {ioe}, v50, %[nge] wave_shr:1 row_mask:0xf bank_mask:0xf")
+    a("v_max3_i32 v53, v46, v45, 0")            # F_A
+    a(f"v_max_i32 v54, {ioe}, {ioh}")           # E_A
+    a("v_max3_i32 v44, v51, v54, v53")          # H_A
+    a("v_subrev_u32 v46, %[GE], v53")           # fhA
+    a("v_subrev_u32 v45, %[GI], v44")           # hgOA
+    a("v_subrev_u32 v54, %[GE], v54")           # E_A - GE
+    a("v_max_i32 v50, v54, v45")                # E_B
+    a("v_max3_i32 v53, v49, v48, 0")            # F_B
+    a("v_max3_i32 v47, v52, v50, v53")          # H_B
+    a("v_subrev_u32 v49, %[GE], v53")           # fhB
+    a("v_subrev_u32 v48, %[GI], v47")           # hgOB
+    a("v_max3_i32 v57, v57, v51, v52")          # M
+
+
+def ring_granule_aff(a):
+    """Publish lanes 32..63 of the I/O pair (the 32 newest outflow rows, row v117) as 16-B
+    granules at their ring slots, rows outside [0, m) dropped."""
+    a("v_mov_b32 v104, v40")
+    a("v_xor_b32 v105, %[ek], v40")
+    a("v_xor_b32 v105, v105, v110")
+    a("v_mov_b32 v106, v41")
+    a("v_xor_b32 v107, %[ek2], v41")
+    a("v_xor_b32 v107, v107, v110")
+    a("v_cmp_gt_u32_e64 s[50:51], %[m], v117")
+    a("s_and_b64 s[50:51], s[50:51], %[lhi]")
+    a("v_cndmask_b32_e64 v109, -16, v108, s[50:51]")
+    a("v_add_u32 v108, 0x200, v108")                    # 32 rows of 16 B on
+    a("v_and_b32 v108, %[gomask16], v108")
+    a("v_add_u32 v110, 0x400, v110")
+    a("v_add_u32 v117, 32, v117")
+    a("buffer_store_dwordx4 v[104:107], v109, %[gors], 0 offen sc1")
+
+
+def ring_gin_check_aff(a):
+    """s[58:59] = live lanes (row k0 + lane < m); s[50:51] = live lanes whose granule fails
+    either half's check."""
+    a("s_sub_i32 s54, %[m], s40")
+    a("v_cmp_gt_i32_e64 s[58:59], s54, %[lane]")
+    a("v_xor_b32 v113, v90, v91")
+    a("v_xor_b32 v113, v113, v112")
+    a("v_cmp_ne_u32_e64 s[56:57], %[ek], v113")
+    a("v_xor_b32 v113, v92, v93")
+    a("v_xor_b32 v113, v113, v112")
+    a("v_cmp_ne_u32_e64 vcc, %[ek2], v113")
+    a("s_or_b64 s[56:57], s[56:57], vcc")
+    a("s_and_b64 s[50:51], s[58:59], s[56:57]")
+    a("s_cmp_lg_u64 s[50:51], 0")
+
+
+def gen_role_ring_aff(IN, OUT_):
+    """gen_role_ring (C = 64, whole-chunk links) around the two-column affine step."""
+    C = 64
+    L = []
+    a = L.append
+    lds_in, lds_out = IN == "lds", OUT_ == "lds"
+    gin, gout = IN == "gran", OUT_ == "gran"
+    ncr = C // 16
+    a("s_nop 4")
+    a("s_waitcnt vmcnt(0) lgkmcnt(0)")
+    for r in ("v44", "v47", "v50", "v57"):
+        a(f"v_mov_b32 {r}, 0")
+    for r in ("v45", "v48", "v40", "v42"):
+        a(f"v_mov_b32 {r}, %[ng]")
+    for r in ("v46", "v49", "v41", "v43"):
+        a(f"v_mov_b32 {r}, %[nge]")
+    a("v_mov_b32 v101, %[raw2]")
+    a("v_mov_b32 v115, %[cro]")
+    a("v_mov_b32 v116, %[rrow]")
+    a("s_mov_b32 s40, 0")
+    a("s_movk_i32 s41, 0")                             # (64 - C) * 8
+    a(f"s_movk_i32 s42, {128 * SZA:#x}")               # ((0 + 128) mod R) * 8
+    a("s_movk_i32 s53, 0xc0")
+    a("s_mov_b32 s45, 0")
+    a("s_mov_b32 s46, 0")
+    a(f"s_movk_i32 s44, {RR}")
+    a("s_mov_b32 s52, 0")
+    if lds_out:
+        a(f"v_mov_b32 v98, {(-64 - C) & 0xffffffff:#x}")
+        a("v_add_u32 v97, s41, %[lout]")
+    if lds_in:
+        a(f"v_mov_b32 v99, {RR + C}")
+        a("v_add_u32 v96, s42, %[lin]")
+    if gout:
+        a("v_mov_b32 v108, %[gooff]")
+        a("v_mov_b32 v110, %[gopos]")
+        a("v_mov_b32 v117, %[gorow]")
+    if gin:
+        a("v_mov_b32 v111, %[gioff]")
+        a("v_mov_b32 v112, %[gipos]")
+        a("buffer_load_dwordx4 v[90:93], v111, %[girs], 0 offen sc1")
+    for q in range(ncr):
+        a(f"ds_read_b128 v[{58 + 4 * q}:{61 + 4 * q}], %[c0]" + (f" offset:{16 * q}" if q else ""))
+    a("s_waitcnt vmcnt(0) lgkmcnt(0)")
+    a("L_loop_%=:")
+    for p in (0, 1):
+        cur = 58 if p == 0 else 74
+        nxt = 74 if p == 0 else 58
+        lds = []
+        if lds_out:
+            if p == 0:
+                a("s_cmp_lt_i32 s44, s40")
+                a(f"s_cbranch_scc1 L_bp{p}_%=")
+                a(f"L_bpr{p}_%=:")
+            a("ds_write_b64 v97, v[40:41]")
+            a("ds_write_b32 %[pout], v98")
+            lds += ["W1", "W2"]
+        if gout:
+            a("s_add_u32 s55, s40, %[bpbase]")
+            a("s_sub_u32 s54, s52, s55")
+            a("s_cmp_lt_i32 s54, 0")
+            a(f"s_cbranch_scc1 L_bpg{p}_%=")
+            a(f"L_bpgr{p}_%=:")
+            ring_granule_aff(a)
+        if lds_in:
+            a("ds_read_b32 v94, %[pin]")
+            a("ds_read_b64 v[90:91], v96")
+            lds += ["A", "B"]
+        stores_after = 2 * gout + (1 if gin and p == 0 else 0)
+        a(f"s_waitcnt vmcnt({stores_after})")
+        if gin:
+            ring_gin_check_aff(a)
+            a(f"s_cbranch_scc1 L_gin{p}_%=")
+            a(f"L_ginr{p}_%=:")
+            a("v_cndmask_b32_e64 v40, %[ng], v90, s[58:59]")
+            a("v_cndmask_b32_e64 v41, %[nge], v92, s[58:59]")
+        elif not lds_in:
+            a("v_mov_b32 v40, %[ng]")
+            a("v_mov_b32 v41, %[nge]")
+        # codes of 64 rows (128..191 ahead of the body's first row) into the wave's code ring
+        a("v_lshrrev_b32 v102, 1, v101")
+        a("v_lshrrev_b32 v113, 2, v101")
+        a("v_xor_b32 v102, v102, v113")
+        a("v_and_or_b32 v102, v102, 3, 4")
+        a("v_cmp_ne_u32_e64 s[56:57], 0, v101")
+        a("v_cndmask_b32_e64 v102, 0, v102, s[56:57]")
+        a("v_add_u32 v103, s53, %[cwr]")
+        a("ds_write_b8 v103, v102")
+        a("s_cmp_eq_u32 s53, 0")
+        a("s_cselect_b32 s54, 0, 64")
+        a("v_add_u32 v103, s54, %[cwm]")
+        a("ds_write_b8 v103, v102")
+        a("s_add_u32 s53, s53, 64")
+        a("s_and_b32 s53, s53, 0xff")
+        lds += ["C1", "C2"]
+        a("v_add_u32 v116, 64, v116")
+        a("buffer_load_ubyte v101, v116, %[rrs], 0 offen")
+        if gin:
+            a(f"v_add_u32 v111, {C * 16:#x}, v111")
+            a("v_and_b32 v111, %[gimask16], v111")
+            a(f"v_add_u32 v112, {C << 5:#x}, v112")
+            a("buffer_load_dwordx4 v[90:93], v111, %[girs], 0 offen sc1")
+            if p == 1:
+                a(f"s_add_u32 s54, s40, {C}")
+                a("s_min_i32 s54, s54, %[m]")
+                a("s_add_u32 s54, s54, %[crv0]")
+                a("v_mov_b32 v114, s54")
+                a("buffer_store_dword v114, %[croff], %[cross], 0 offen sc1")
+        a("v_add_u32 v95, %[cbase], v115")
+        for q in range(ncr):
+            a(f"ds_read_b128 v[{nxt + 4 * q}:{nxt + 4 * q + 3}], v95 offset:{16 * q}" if q else
+              f"ds_read_b128 v[{nxt}:{nxt + 3}], v95")
+        a(f"v_add_u32 v115, {C}, v115")
+        a("v_and_b32 v115, 0xff, v115")
+        lds += ["N%d" % q for q in range(ncr)]
+        if lds_in:
+            after_a = len(lds) - 1 - lds.index("A")
+            a(f"s_waitcnt lgkmcnt({after_a})")
+            a("v_readfirstlane_b32 s43, v94")
+            a("s_cmp_lt_i32 s43, s40")
+            a(f"s_cbranch_scc1 L_in{p}_%=")
+            a(f"L_inr{p}_%=:")
+            a(f"s_waitcnt lgkmcnt({after_a - 1})")
+            a("v_mov_b32 v40, v90")
+            a("v_mov_b32 v41, v91")
+            a("ds_write_b32 %[qme], v99")
+        else:
+            a(f"s_waitcnt lgkmcnt({len(lds)})")
+        for u in range(C // 4):
+            a(f"v_perm_b32 v55, %[pA], %[k80], v{cur + u}")
+            a(f"v_perm_b32 v56, %[pB], %[k80], v{cur + u}")
+            for b in range(4):
+                step_aff2(a, b, b % 2 == 0)
+            if gout and u == 7:
+                ring_granule_aff(a)
+        a(f"s_add_i32 s40, s40, {C}")
+        if lds_out:
+            a(f"s_add_u32 s41, s41, {SZA * C:#x}")
+            a(f"s_and_b32 s41, s41, {(RR - 1) * SZA:#x}")
+            a("v_add_u32 v97, s41, %[lout]")
+            a(f"v_add_u32 v98, {C}, v98")
+        if lds_in:
+            a(f"s_add_u32 s42, s42, {SZA * C:#x}")
+            a(f"s_and_b32 s42, s42, {(RR - 1) * SZA:#x}")
+            a("v_add_u32 v96, s42, %[lin]")
+            a(f"v_add_u32 v99, {C}, v99")
+    a("s_cmp_lt_i32 s40, %[end]")
+    a("s_cbranch_scc1 L_loop_%=")
+    if lds_out:
+        a("s_cmp_lt_i32 s44, s40")
+        a("s_cbranch_scc1 L_bpx_%=")
+        a("L_bpxr_%=:")
+        a("ds_write_b64 v97, v[40:41]")
+        a(f"v_mov_b32 v98, {BIG:#x}")
+        a("ds_write_b32 %[pout], v98")
+    if gout:
+        a("s_add_u32 s55, s40, %[bpbase]")
+        a("s_sub_u32 s54, s52, s55")
+        a("s_cmp_lt_i32 s54, 0")
+        a("s_cbranch_scc1 L_bpgx_%=")
+        a("L_bpgxr_%=:")
+        ring_granule_aff(a)
+    if gin:
+        a("s_add_u32 s54, %[m], %[crv0]")
+        a("v_mov_b32 v114, s54")
+        a("buffer_store_dword v114, %[croff], %[cross], 0 offen sc1")
+    a("s_waitcnt vmcnt(0) lgkmcnt(0)")
+    a("v_mov_b32 %[M], v57")
+    a("s_mov_b32 %[fail], s45")
+    a("s_mov_b32 %[slow], s46")
+    a("s_branch L_done_%=")
+    if lds_in:
+        for p in (0, 1):
+            slow_wait(a, f"L_in{p}_%=", f"L_inr{p}_%=", "v94", "%[pin]", "s43", reread="ds_read_b64 v[90:91], v96")
+    if lds_out:
+        slow_wait(a, "L_bp0_%=", "L_bpr0_%=", "v100", "%[qnx]", "s44")
+        slow_wait(a, "L_bpx_%=", "L_bpxr_%=", "v100", "%[qnx]", "s44")
+    if gout:
+        for lab, res in (("L_bpg0_%=", "L_bpgr0_%="), ("L_bpg1_%=", "L_bpgr1_%="), ("L_bpgx_%=", "L_bpgxr_%=")):
+            slow_bp_hbm_aff(a, lab, res)
+    if gin:
+        for p in (0, 1):
+            slow_gin_aff(a, f"L_gin{p}_%=", f"L_ginr{p}_%=")
+    a("L_done_%=:")
+    return L
+
+
+def slow_bp_hbm_aff(a, label, resume):
+    a(f"{label}:")
+    a("s_add_u32 s46, s46, 1")
+    a("s_cmp_lg_u32 s45, 0")
+    a(f"s_cbranch_scc1 {resume}")
+    a(f"{label}_w:")
+    a("buffer_load_dword v100, off, %[bpr], 0 sc1")
+    a("s_memrealtime s[48:49]")
+    a("s_waitcnt vmcnt(0) lgkmcnt(0)")
+    a("v_readfirstlane_b32 s52, v100")
+    a("s_add_u32 s55, s40, %[bpbase]")
+    a("s_sub_u32 s54, s52, s55")
+    a("s_cmp_ge_i32 s54, 0")
+    a(f"s_cbranch_scc1 {resume}")
+    slow_timeout(a, label)
+    a(f"{label}_x:")
+    a("s_mov_b32 s45, 1")
+    a(f"s_branch {resume}")
+
+
+def slow_gin_aff(a, label, resume):
+    a(f"{label}:")
+    a("s_add_u32 s46, s46, 1")
+    a("s_cmp_lg_u32 s45, 0")
+    a(f"s_cbranch_scc1 {resume}")
+    a(f"{label}_w:")
+    a("buffer_load_dwordx4 v[90:93], v111, %[girs], 0 offen sc1")
+    a("s_memrealtime s[48:49]")
+    a("s_waitcnt vmcnt(0) lgkmcnt(0)")
+    ring_gin_check_aff(a)
+    a(f"s_cbranch_scc0 {resume}")
+    slow_timeout(a, label)
+    a(f"{label}_x:")
+    a("s_mov_b32 s45, 1")
+    a(f"s_branch {resume}")
+
+
+CLOBBERS_RING_AFF = ['"v%d"' % r for r in range(40, 118)] + \
+    ['"s%d"' % r for r in range(40, 60) if r not in (47,)] + ['"scc"', '"vcc"', '"memory"']
+OUT_RING_AFF = os.path.join(ROOT, "concurrentproject_amd", "csrc", "sw_flow3ra_loops.inc")
+
+
+def emit_ring_aff():
+    out = ["// GENERATED by tools/gen_flow3.py -- do not edit.  The flow3 ring-mode affine-step chunk loops",
+           "// (sw_flow3.hip sw_flow3ra_kernel): one inline-asm block per strip role, C = 64, R = %d rows of 8-B slots." % RR,
+           "// Operands: see F3RALoop in sw_flow3.hip; fixed registers: tools/gen_flow3.py (gen_role_ring_aff).",
+           "#pragma once", ""]
+    for IN, OUT_ in [(i, o) for i in ROLES_IN_RING for o in ROLES_OUT]:
+        body = gen_role_ring_aff(IN, OUT_)
+        out.append("template <> __device__ __forceinline__ F3Res f3ra_loop<F3_%s, F3_%s>(const F3RALoop& x) {"
+                   % (IN.upper(), OUT_.upper()))
+        out.append("    F3Res r;")
+        out.append("    asm volatile(")
+        for line in body:
+            out.append('        "%s\\n\\t"' % line)
+        out.append('        : [M] "=v"(r.M), [fail] "=s"(r.fail), [slow] "=s"(r.slow)')
+        out.append('        : [pA] "v"(x.pA), [pB] "v"(x.pB), [ng] "v"(x.ng), [nge] "v"(x.nge), [GI] "s"(x.GI),')
+        out.append('          [GE] "s"(x.GE), [k80] "s"(x.k80), [m] "s"(x.m), [end] "s"(x.end), [dlo] "s"(x.dlo),')
+        out.append('          [dhi] "s"(x.dhi), [lane] "v"(x.lane), [raw2] "v"(x.raw2), [cro] "v"(x.cro), [c0] "v"(x.c0),')
+        out.append('          [cbase] "v"(x.cbase), [cwr] "v"(x.cwr), [cwm] "v"(x.cwm), [rrs] "s"(x.rrs), [rrow] "v"(x.rrow),')
+        out.append('          [lin] "v"(x.lin), [lout] "v"(x.lout), [pin] "v"(x.pin), [pout] "v"(x.pout),')
+        out.append('          [qme] "v"(x.qme), [qnx] "v"(x.qnx),')
+        out.append('          [girs] "s"(x.girs), [gioff] "v"(x.gioff), [gipos] "v"(x.gipos), [gimask16] "s"(x.gimask16),')
+        out.append('          [ek] "s"(x.ek), [ek2] "s"(x.ek2), [cross] "s"(x.cross), [crv0] "s"(x.crv0), [croff] "v"(x.croff),')
+        out.append('          [gors] "s"(x.gors), [gooff] "v"(x.gooff), [gopos] "v"(x.gopos), [gomask16] "s"(x.gomask16),')
+        out.append('          [gorow] "v"(x.gorow), [lhi] "s"(x.lhi), [bpr] "s"(x.bpr), [bpbase] "s"(x.bpbase)')
+        out.append("        : " + ", ".join(CLOBBERS_RING_AFF) + ");")
+        out.append("    return r;")
+        out.append("}")
+        out.append("")
+    return "\n".join(out)
+
 
 def main():
     spec = int(os.environ.get("F3_SPEC", "4"))
     halfpub = os.environ.get("F3_HALFPUB", "1") != "0"
     text = emit(spec, halfpub)
     text_ring = emit_ring()
+    text_aff = emit_aff()
+    text_ring_aff = emit_ring_aff()
     if "--check" in sys.argv:
         cur = open(OUT).read() if os.path.exists(OUT) else ""
         cur_r = open(OUT_RING).read() if os.path.exists(OUT_RING) else ""
-        sys.exit(0 if cur == text and cur_r == text_ring else 1)
+        cur_a = open(OUT_AFF).read() if os.path.exists(OUT_AFF) else ""
+        cur_ra = open(OUT_RING_AFF).read() if os.path.exists(OUT_RING_AFF) else ""
+        sys.exit(0 if cur == text and cur_r == text_ring and cur_a == text_aff and cur_ra == text_ring_aff else 1)
+    with open(OUT_AFF, "w") as f:
+        f.write(text_aff)
+    with open(OUT_RING_AFF, "w") as f:
+        f.write(text_ring_aff)
     path = OUT
     for i, arg in enumerate(sys.argv):
         if arg == "-o":
