@@ -127,6 +127,7 @@ def gen_role(IN, OUT_, spec=0, halfpub=True, C=32, hl=False):
     if lds_in and spec:
         a("ds_read_b32 v93, %[pin]")
         a("ds_read_b32 v92, v95")
+    a(".p2align 6")                # the chunk loop on a 64-B boundary (a lone wave's issue rate depends on it)
     a("L_loop_%=:")
     for p in (0, 1):
         cur = 76 if p == 0 else 84
@@ -415,6 +416,7 @@ def gen_role_ring(IN, OUT_, C=64, hl=False):
     for q in range(ncr):
         a(f"ds_read_b128 v[{52 + 4 * q}:{55 + 4 * q}], %[c0]" + (f" offset:{16 * q}" if q else ""))
     a("s_waitcnt vmcnt(0) lgkmcnt(0)")
+    a(".p2align 6")                # the chunk loop on a 64-B boundary (a lone wave's issue rate depends on it)
     a("L_loop_%=:")
     for p in (0, 1):
         cur = 52 if p == 0 else 68
@@ -807,6 +809,7 @@ def gen_role_aff(IN, OUT_, C=32, hl=True):
     if lds_in:
         a("ds_read_b32 v98, %[pin]")
         a("ds_read_b64 v[96:97], v100")
+    a(".p2align 6")                # the chunk loop on a 64-B boundary (a lone wave's issue rate depends on it)
     a("L_loop_%=:")
     for p in (0, 1):
         cur = 80 if p == 0 else 88
@@ -1066,6 +1069,7 @@ def gen_role_ring_aff(IN, OUT_):
     for q in range(ncr):
         a(f"ds_read_b128 v[{58 + 4 * q}:{61 + 4 * q}], %[c0]" + (f" offset:{16 * q}" if q else ""))
     a("s_waitcnt vmcnt(0) lgkmcnt(0)")
+    a(".p2align 6")                # the chunk loop on a 64-B boundary (a lone wave's issue rate depends on it)
     a("L_loop_%=:")
     for p in (0, 1):
         cur = 58 if p == 0 else 74

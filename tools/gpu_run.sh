@@ -9,6 +9,8 @@
 #   bench[:ARGS]        bench.py ARGS (words joined by +), JSON line to gpurun_out/bench_<n>.json
 #   prof:WHICH          tools/prof_round.sh WHICH (c2 c3 c5 c5p8 ...; words joined by +)
 #   harness             the reference's TestFileWithGPU against the library
+#   smoke               __graft_entry__.smoke()
+#   ab:REPS:V1:V2...    tools/ab.sh REPS V1 V2 ... (V = label=bench args, words joined by +)
 set -e -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
@@ -46,6 +48,15 @@ for st in "$@"; do
       timeout -k 10 300 python -u -m pytest tests/test_harness.py -m gpu -x -q --timeout 250 --timeout-method thread \
         > gpurun_out/harness_$n.log 2>&1 || { tail -20 gpurun_out/harness_$n.log; exit 1; }
       tail -2 gpurun_out/harness_$n.log ;;
+    smoke)
+      timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$n.log 2>&1 \
+        || { tail -20 gpurun_out/smoke_$n.log; exit 1; }
+      tail -2 gpurun_out/smoke_$n.log ;;
+    ab)
+      reps=${rest%%:*}; vs=${rest#*:}
+      IFS=':' read -ra V <<< "$vs"
+      args=(); for v in "${V[@]}"; do args+=("${v//+/ }"); done
+      bash tools/ab.sh "$reps" "${args[@]}" ;;
     *) echo "unknown step $st"; exit 2 ;;
   esac
 done

@@ -41,6 +41,8 @@ def main():
     sw.set_option("W", W)
     sw.set_option("C", C)
     sw.set_option("f2w", f2w)
+    if os.environ.get("TRACE_PARAMS"):   # MATCH,MISMATCH,G_INIT,G_EXT
+        sw.set_params(sw.Params(*(int(x) for x in os.environ["TRACE_PARAMS"].split(","))))
     for kv in os.environ.get("TRACE_OPTS", "").split():   # extra engine options k=v
         k, v = kv.split("=")
         sw.set_option(k, int(v))
