@@ -111,8 +111,9 @@ def lib() -> ctypes.CDLL:
     L.sw_score_batch_multi.restype = i
     L.sw_batch_shard.argtypes = [i, i, i, ctypes.POINTER(i), ctypes.POINTER(i)]
     L.sw_batch_shard.restype = i
-    L.sw_batch_gather_plan.argtypes = [i, i, ctypes.POINTER(i), ctypes.POINTER(i)]
-    L.sw_batch_gather_plan.restype = i
+    if hasattr(L, "sw_batch_gather_plan"):   # (absent from pre-r05 builds that tools/ab.sh --libs may load)
+        L.sw_batch_gather_plan.argtypes = [i, i, ctypes.POINTER(i), ctypes.POINTER(i)]
+        L.sw_batch_gather_plan.restype = i
     L.sw_score_batch_device.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(i),
                                         ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(i), i, ctypes.c_void_p, i,
                                         ctypes.c_void_p]

@@ -5,7 +5,7 @@
 #   bash tools/ab.sh REPS "label=bench args" "label=bench args" ...
 #       e.g. bash tools/ab.sh 3 "hl1=--no-extra --opt f3hl=1" "hl0=--no-extra --opt f3hl=0"
 #            bash tools/ab.sh 2 "c5=--workload slab --steps 3" "wgs3=--workload slab --steps 3 --opt f2_wgs=3"
-#   bash tools/ab.sh REPS --libs libA.so libB.so [bench args]     (two library builds, SWMI355_LIB)
+#   bash tools/ab.sh REPS --libs libA.so libB.so ... -- [bench args]   (library builds, SWMI355_LIB)
 # Every run has its own time limit; the first failing run ends the script.
 set -e -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -18,9 +18,11 @@ run() {  # label, env, args...
 }
 for i in $(seq 1 $reps); do
   if [ "$1" = "--libs" ]; then
-    A=$2; B=$3
-    run A "SWMI355_LIB=$A" "${@:4}"
-    run B "SWMI355_LIB=$B" "${@:4}"
+    libs=(); shift_n=1
+    for x in "${@:2}"; do shift_n=$((shift_n + 1)); [ "$x" = "--" ] && break; libs+=("$x"); done
+    for L in "${libs[@]}"; do
+      run "$(basename $L .so)" "SWMI355_LIB=$L" "${@:$((shift_n + 1))}"
+    done
   else
     for v in "$@"; do
       run "${v%%=*}" "" ${v#*=}

@@ -42,7 +42,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(ROOT, "concurrentproject_amd", "csrc", "sw_flow3_loops.inc")
 
 ROLES_IN = ("none", "lds")
-MID_AHEAD = int(os.environ.get("F3_MIDAHEAD", "1"))   # 4-step groups the mid-chunk inflow read runs ahead
+MID_AHEAD = int(os.environ.get("F3_MIDAHEAD", "1"))
+LOOP_PAD = int(os.environ.get("F3_LOOP_PAD", "0"))   # 4-B s_nop 0 between the 64-B boundary and the loop (A/B)   # 4-step groups the mid-chunk inflow read runs ahead
 ROLES_OUT = ("none", "lds", "gran")
 
 
@@ -64,6 +65,86 @@ def step(a, io, l0, b, r=STAGED):
     a(f"v_max3_i32 {r['HB']}, {r['HGO']}, {r['HGOB']}, {r['TB']}")
     a(f"v_sub_u32_e64 {r['HGOB']}, {r['HB']}, %[G] clamp")
     a(f"v_max3_i32 {r['M']}, {r['M']}, {r['TA']}, {r['TB']}")
+
+
+
+# ---- 8-byte alignment of the chunk loops ----------------------------------------------------
+# A lone wave issues an 8-byte instruction (VOP3, DPP, SDWA, DS, buffer, VOP2 + literal) more
+# slowly when it sits at an address = 4 mod 8: C2's flow3 kernel ran 2.76 ms with 82 % of its
+# main loop's 8-B instructions there and 2.545 ms with 18 % (the same code shifted by one 4-B
+# s_nop; profiles/r05_ab_align.md).  So every loop is laid out from its 64-B aligned label with
+# all 8-B instructions on 8-B boundaries: before an 8-B instruction that would land at 4 mod 8,
+# the nearest 4-B VOP1/VOP2 instruction since the previous 8-B one is re-encoded as VOP3 (_e64,
+# 8 B, same operation), or, when that run holds none (SALU, waits), one s_nop 0 is inserted.
+# Instruction sizes come from llvm-mc (gfx950), with each operand placeholder replaced by a
+# register of its class.  Staged loops only: the ring loops (4 waves per SIMD, issue-bound)
+# measured 1.5 % slower aligned (C5 166.6 -> 168.7 ms), the nops costing issue slots there.
+LLVM_MC = "/opt/rocm/lib/llvm/bin/llvm-mc"
+OPERAND_CLASS = {
+    "rsrc": "s[0:3]", "rrs": "s[0:3]", "girs": "s[0:3]", "gors": "s[0:3]", "cross": "s[0:3]", "bpr": "s[0:3]",
+    "m48": "s[0:1]", "lhi": "s[0:1]",
+    "G": "s0", "GI": "s0", "GE": "s0", "k80": "s0", "end": "s0", "dlo": "s0", "dhi": "s0", "ek": "s0", "ek2": "s0",
+    "m": "s0", "gimask8": "s0", "gomask8": "s0", "gimask16": "s0", "gomask16": "s0", "crv0": "s0", "bpbase": "s0",
+    "fail": "s0", "slow": "s0",
+}
+_SIZE_CACHE = {}
+_PROMOTABLE = ("v_mov_b32", "v_add_u32", "v_sub_u32", "v_subrev_u32", "v_xor_b32", "v_max_i32", "v_max_u32",
+               "v_min_i32", "v_lshrrev_b32", "v_lshlrev_b32", "v_and_b32", "v_or_b32", "v_cndmask_b32")
+
+
+def _norm(line):
+    import re
+    return re.sub(r"%\[(\w+)\]", lambda m: OPERAND_CLASS.get(m.group(1), "v0"), line).replace("%=", "0")
+
+
+def _is_code(line):
+    t = line.strip()
+    return t and not t.endswith(":") and not t.startswith(".")
+
+
+def _sizes(lines):
+    import re
+    import subprocess
+    todo = sorted({_norm(l) for l in lines if _is_code(l) and not l.startswith(("s_cbranch", "s_branch"))} -
+                  set(_SIZE_CACHE))
+    if todo:
+        r = subprocess.run([LLVM_MC, "-arch=amdgcn", "-mcpu=gfx950", "-show-encoding"], input="\n".join(todo) + "\n",
+                           capture_output=True, text=True, check=True)
+        enc = [l for l in r.stdout.splitlines() if "encoding:" in l]
+        assert len(enc) == len(todo), (len(enc), len(todo), r.stderr[:2000])
+        for t, e in zip(todo, enc):
+            _SIZE_CACHE[t] = len(re.search(r"encoding: \[(.*)\]", e).group(1).split(","))
+    return [0 if not _is_code(l) else 4 if l.startswith(("s_cbranch", "s_branch")) else _SIZE_CACHE[_norm(l)]
+            for l in lines]
+
+
+def align8(lines):
+    """The loop of an asm block (from its 64-B aligned L_loop label to the loop's back branch)
+    with every 8-B instruction on an 8-B boundary (see above)."""
+    try:
+        i0 = lines.index("L_loop_%=:")
+        i1 = lines.index("s_cbranch_scc1 L_loop_%=")
+    except ValueError:
+        return lines
+    body = lines[i0 + 1:i1]
+    sz = _sizes(body)
+    out, off, cand = [], 0, None        # cand: index in out of the last promotable 4-B VALU since an 8-B one
+    for l, n in zip(body, sz):
+        if n == 8 and off % 8 == 4:
+            if cand is not None:
+                op, rest = out[cand].split(" ", 1)
+                out[cand] = op + "_e64 " + rest
+            else:
+                out.append("s_nop 0")
+            off += 4
+            cand = None
+        out.append(l)
+        off += n
+        if n == 8:
+            cand = None
+        elif n == 4 and l.split(" ", 1)[0] in _PROMOTABLE:
+            cand = len(out) - 1
+    return lines[:i0 + 1] + out + lines[i1:]
 
 
 def granule(a, rows):
@@ -128,6 +209,8 @@ def gen_role(IN, OUT_, spec=0, halfpub=True, C=32, hl=False):
         a("ds_read_b32 v93, %[pin]")
         a("ds_read_b32 v92, v95")
     a(".p2align 6")                # the chunk loop on a 64-B boundary (a lone wave's issue rate depends on it)
+    for _ in range(LOOP_PAD):
+        a("s_nop 0")
     a("L_loop_%=:")
     for p in (0, 1):
         cur = 76 if p == 0 else 84
@@ -292,7 +375,7 @@ def emit(spec=0, halfpub=True):
     for C, hl in ((32, 0), (16, 0), (32, 1)):
         for IN in ROLES_IN:
             for OUT_ in ROLES_OUT:
-                body = gen_role(IN, OUT_, spec, halfpub, C, bool(hl))
+                body = align8(gen_role(IN, OUT_, spec, halfpub, C, bool(hl)))
                 out.append("template <> __device__ __forceinline__ F3Res f3_loop<%d, %d, F3_%s, F3_%s>(const F3Loop& x) {"
                            % (C, hl, IN.upper(), OUT_.upper()))
                 out.append("    F3Res r;")
@@ -417,6 +500,8 @@ def gen_role_ring(IN, OUT_, C=64, hl=False):
         a(f"ds_read_b128 v[{52 + 4 * q}:{55 + 4 * q}], %[c0]" + (f" offset:{16 * q}" if q else ""))
     a("s_waitcnt vmcnt(0) lgkmcnt(0)")
     a(".p2align 6")                # the chunk loop on a 64-B boundary (a lone wave's issue rate depends on it)
+    for _ in range(LOOP_PAD):
+        a("s_nop 0")
     a("L_loop_%=:")
     for p in (0, 1):
         cur = 52 if p == 0 else 68
@@ -810,6 +895,8 @@ def gen_role_aff(IN, OUT_, C=32, hl=True):
         a("ds_read_b32 v98, %[pin]")
         a("ds_read_b64 v[96:97], v100")
     a(".p2align 6")                # the chunk loop on a 64-B boundary (a lone wave's issue rate depends on it)
+    for _ in range(LOOP_PAD):
+        a("s_nop 0")
     a("L_loop_%=:")
     for p in (0, 1):
         cur = 80 if p == 0 else 88
@@ -919,7 +1006,7 @@ def emit_aff():
     for C, hl in ((32, 1), (32, 0), (16, 0)):
         for IN in ROLES_IN:
             for OUT_ in ROLES_OUT:
-                body = gen_role_aff(IN, OUT_, C, bool(hl))
+                body = align8(gen_role_aff(IN, OUT_, C, bool(hl)))
                 out.append("template <> __device__ __forceinline__ F3Res f3a_loop<%d, %d, F3_%s, F3_%s>(const F3ALoop& x) {"
                            % (C, hl, IN.upper(), OUT_.upper()))
                 out.append("    F3Res r;")
@@ -1070,6 +1157,8 @@ def gen_role_ring_aff(IN, OUT_):
         a(f"ds_read_b128 v[{58 + 4 * q}:{61 + 4 * q}], %[c0]" + (f" offset:{16 * q}" if q else ""))
     a("s_waitcnt vmcnt(0) lgkmcnt(0)")
     a(".p2align 6")                # the chunk loop on a 64-B boundary (a lone wave's issue rate depends on it)
+    for _ in range(LOOP_PAD):
+        a("s_nop 0")
     a("L_loop_%=:")
     for p in (0, 1):
         cur = 58 if p == 0 else 74
