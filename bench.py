@@ -267,7 +267,9 @@ def kernel_label(st):
         ring, w2, f3, hl, aff3 = bool(v & 4), bool(v & 16), bool(v & 64), bool(v & 512), bool(v & 1024)
         if f3 or aff3:
             name = ("flow3 ring" if ring else "flow3") + (" affine" if aff3 else "")
-            fn = ("sw_flow3r" if ring else "sw_flow3") + ("a" if aff3 else "") + "_kernel"
+            fn = ("sw_flow3r" if ring else "sw_flow3") + ("a" if aff3 else "") + ("s" if v & 2048 else "") + "_kernel"
+            if v & 2048:
+                name += ", column slab (peer edges)"
         else:
             name = "flow2 " + ("pair per workgroup" if v & 32 else "ring" if ring else "streamed" if v & 2 else "staged")
             fn = "sw_flow2_kernel"

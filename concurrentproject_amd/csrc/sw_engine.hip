@@ -65,7 +65,7 @@ Params g_params;
 std::atomic<long long> g_opt_W{0}, g_opt_C{0}, g_opt_bytes{0}, g_opt_timeout{30}, g_opt_blocks{0}, g_opt_orient{0},
     g_opt_mode{-1}, g_opt_trace{0}, g_opt_duo_f16{1}, g_opt_f2stream{0}, g_opt_ring{-1}, g_opt_ring_rows{4096}, g_opt_f2_wgs{0}, g_opt_f2w{0}, g_opt_f2pwg{-1},
     g_opt_linear{-1}, g_opt_f3{1}, g_opt_slab_plain{0}, g_opt_duo_lds{1}, g_opt_duo_tab{1}, g_opt_duo_roles{1}, g_opt_f3hl{1},
-    g_opt_f3rhl{0}, g_opt_f3a{1};
+    g_opt_f3rhl{0}, g_opt_f3a{1}, g_opt_f3slab{1};
 
 // Longest sequence the engine takes: granule buffers of m rows keep m * 16 in the
 // 32-bit record count of a buffer resource (sw_device.h linear_edge).
@@ -458,6 +458,15 @@ int finalize_mode(Job& job, const Params& prm, int cus) {
                 plan_flow2(w2, true);
                 if (w2.ring) job = w2;
             }
+            // a column slab (f-1) runs flow3's ring kernel with its slab roles (sw_flow3rs_kernel /
+            // sw_flow3ras_kernel): two columns per lane, ring edges between its own groups (forced
+            // for any size; with one group there are none), option f3slab = 0 keeps flow2's slab kernel
+            const bool lin = prm.gap_init == prm.gap_ext && g_opt_linear.load() != 0;
+            if (job.slab && g_opt_f3slab.load() != 0 && (lin ? g_opt_f3.load() != 0 : g_opt_f3a.load() != 0) &&
+                g_opt_f2w.load() != 1 && g_opt_ring.load() != 0 && (g_opt_C.load() == 0 || g_opt_C.load() == 64)) {
+                if (!job.f2w2) plan_flow2(job, true);
+                job.ring = true;
+            }
             job.f2_stream = job.ring || !flow2_staged(job, max_m);   // ring mode runs with streamed codes
             // ring mode (one pair of many groups per CU, C5): throughput-bound, so 64-row chunks
             // (half the per-chunk work per step) beat the shorter hand-off lag of 32 (C5 249 -> 220 ms)
@@ -674,8 +683,9 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
     int max_m_f3 = 0;
     for (const PairDesc& d : job.pairs) max_m_f3 = std::max(max_m_f3, d.m);
     const bool f3_base = g_opt_f3.load() != 0 && job.mode == MODE_FLOW2 && job.f2w2 && f2_lin && !job.pwg;
+    const bool f3_slab_ok = edge == nullptr || (g_opt_f3slab.load() != 0 && job.C == 64);
     const bool use_f3 = f3_base && ((!f2s && !job.ring && flow3_fits(max_m_f3, job.C)) ||
-                                    (job.ring && edge == nullptr && (job.C == 64 || job.C == 32)));
+                                    (job.ring && f3_slab_ok && (job.C == 64 || job.C == 32)));
     // the general affine step (G_INIT != G_EXT, or option linear = 0) on flow3's staged kernel:
     // one column per lane, rows in LDS, linear edges (C2 with affine constants); option f3a = 0
     // keeps flow2
@@ -684,7 +694,7 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
                          flow3_fits(max_m_f3, job.C, true);
     // ... and in ring mode at two columns per lane (finalize_mode planned the strips for it)
     const bool use_f3ra = g_opt_f3a.load() != 0 && job.mode == MODE_FLOW2 && job.f2w2 && !f2_lin && !job.pwg &&
-                          job.ring && edge == nullptr && job.C == 64;
+                          job.ring && f3_slab_ok && job.C == 64;
     // duo batches at C = 64: strip hand-offs in LDS when the wrap buffer (a round's rows of
     // both pairs) fits the default dynamic-LDS limit; no boundary buffers in HBM then
     // and, at 4 or 8 columns per lane, the row codes from an LDS table when both fit two workgroups per CU
@@ -719,6 +729,8 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
         probe.f2_w2 = job.f2w2;
         probe.f3_hl = use_f3 && job.C == 64 && g_opt_f3rhl.load() != 0;
         probe.f3ra = use_f3ra;
+        probe.f3_slab = (use_f3 || use_f3ra) && edge != nullptr;
+        if (probe.f3_slab) probe.f3_hl = false;
         int fit = 0;
         for (;; --f2_wgs) {
             probe.f2_wgs = f2_wgs;
@@ -793,6 +805,8 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
                            (job.ring && job.C == 64 && g_opt_f3rhl.load() != 0));
     cfg.f3a = use_f3a;
     cfg.f3ra = use_f3ra;
+    cfg.f3_slab = (use_f3 || use_f3ra) && edge != nullptr;
+    if (cfg.f3_slab) cfg.f3_hl = false;   // (the slab roles exist at C = 64, whole-chunk links)
     if (use_f3a) cfg.f3_hl = job.C == 32 && g_opt_f3hl.load() != 0;
     cfg.duo_wrap = duo_wrap;
     cfg.duo_tab = duo_tab;
@@ -891,7 +905,8 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
     t_stats.mode = job.mode;
     t_stats.variant = (cfg.duo_f16 ? 1 : 0) | (cfg.f2_stream ? 2 : 0) | (job.ring ? 4 : 0) | (cfg.f2_lin ? 8 : 0) |
                       (cfg.f2_w2 ? 16 : 0) | (cfg.f2_pwg ? 32 : 0) | (cfg.f3 ? 64 : 0) | (cfg.duo_wrap > 0 ? 128 : 0) |
-                      (cfg.duo_tab > 0 ? 256 : 0) | (cfg.f3_hl ? 512 : 0) | (cfg.f3a || cfg.f3ra ? 1024 : 0);
+                      (cfg.duo_tab > 0 ? 256 : 0) | (cfg.f3_hl ? 512 : 0) | (cfg.f3a || cfg.f3ra ? 1024 : 0) |
+                      (cfg.f3_slab ? 2048 : 0);
     t_stats.boundary_bytes = (long long)(job.bnd_granules * sizeof(Granule));
     c->last = s;
     return 0;
@@ -1717,6 +1732,9 @@ int sw_set_option(const char* key, long long v) {
     } else if (k == "f3rhl") {   // 1: flow3 ring launches at C = 64 with half-chunk in-workgroup links
         if (v < 0 || v > 1) return -1;
         g_opt_f3rhl = v;
+    } else if (k == "f3slab") {   // 1 (default): column slabs on flow3's ring kernel (sw_flow3rs_kernel), 0: flow2
+        if (v < 0 || v > 1) return -1;
+        g_opt_f3slab = v;
     } else if (k == "f3a") {   // 1 (default): staged affine-step launches on flow3 (sw_flow3a_kernel), 0: flow2
         if (v < 0 || v > 1) return -1;
         g_opt_f3a = v;
@@ -1770,6 +1788,7 @@ long long sw_get_option(const char* key) {
     if (k == "f3hl") return g_opt_f3hl;
     if (k == "f3rhl") return g_opt_f3rhl;
     if (k == "f3a") return g_opt_f3a;
+    if (k == "f3slab") return g_opt_f3slab;
     return -1;
 }
 

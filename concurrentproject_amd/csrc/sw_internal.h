@@ -137,6 +137,7 @@ struct LaunchCfg {
     bool f3_hl = false;     // flow3 staged at C = 32: in-workgroup links hand off every half chunk
     bool f3a = false;       // MODE_FLOW2 staged one-column launch with the affine step on flow3 (sw_flow3a_kernel)
     bool f3ra = false;      // MODE_FLOW2 ring-mode two-column launch with the affine step on flow3 (sw_flow3ra_kernel)
+    bool f3_slab = false;   // flow3 ring launch of a column slab (sw_flow3rs_kernel / sw_flow3ras_kernel)
     int duo_wrap = 0;       // MODE_DUO at C = 64: > 0 = strip hand-offs in LDS (sw_duo_lds_kernel), this many
                             // wrap-buffer slots (a power of two >= every m_pad); 0 = HBM granules
     int duo_tab = 0;        // with duo_wrap, W % 4 == 0: > 0 = row codes from an LDS table of this many words

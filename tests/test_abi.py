@@ -119,7 +119,8 @@ def test_slab_edges_are_system_scope():
     """Cross-GPU slab edges are loaded and stored system scope (sc0 sc1: the LLVM
     memory model's relaxed system-scope atomic on gfx950); in-GPU edges device
     scope (sc1 only).  Checked on the built code object's disassembly (the
-    flow2 kernel template <C, STREAM, RING, SLAB, LIN>, sw_flow2.hip)."""
+    flow2 kernel template <C, STREAM, RING, SLAB, LIN>, sw_flow2.hip, and flow3's
+    slab kernels sw_flow3rs_kernel / sw_flow3ras_kernel, sw_flow3.hip)."""
     import re
     import tempfile
     sys.path.insert(0, os.path.join(ROOT, "tools"))
@@ -158,3 +159,22 @@ def test_slab_edges_are_system_scope():
             assert not sys_ops, (name, sys_ops[:3])
             assert all(" sc1" in x for x in g_stores), name
     assert seen[0] >= 6 and seen[1] >= 3 and pwg >= 2, (seen, pwg)
+    # flow3 (sw_flow3.hip): the slab instantiations of the ring kernel (linear-gap 8-B and affine
+    # 16-B granules) load and store their peer edges system scope; every other flow3 kernel
+    # (staged, ring, affine) keeps its granules device scope
+    f3 = {0: 0, 1: 0}
+    for name, body in funcs.items():
+        m = re.search(r"sw_flow3(r|ra|rs|ras|a)?_kernel", name)
+        if not m:
+            continue
+        slab = m.group(1) in ("rs", "ras")
+        g_ops = [x for x in body if x.startswith(("buffer_load_dwordx2", "buffer_load_dwordx4",
+                                                    "buffer_store_dwordx2", "buffer_store_dwordx4"))]
+        sys_ops = [x for x in g_ops if "sc0 sc1" in x]
+        if slab:
+            assert any(x.startswith("buffer_load") for x in sys_ops), name
+            assert any(x.startswith("buffer_store") for x in sys_ops), name
+        else:
+            assert not sys_ops, (name, sys_ops[:3])
+        f3[slab] += 1
+    assert f3[1] == 2 and f3[0] >= 8, f3

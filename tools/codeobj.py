@@ -63,11 +63,15 @@ def disassemble(path, out_dir):
 
 
 def functions(text):
-    """{symbol: [instruction lines]} of an llvm-objdump -d listing."""
+    """{symbol: [instruction lines]} of an llvm-objdump -d listing.  Local labels of inline asm
+    (L_loop_N, L_done_N, ... in the flow3 chunk loops) stay part of the enclosing function."""
     out, cur = {}, None
     for line in text.splitlines():
         if line.endswith(">:") and "<" in line:
-            cur = line[line.index("<") + 1:-2]
+            name = line[line.index("<") + 1:-2]
+            if name.startswith("L_") and cur is not None:
+                continue
+            cur = name
             out[cur] = []
         elif cur is not None and line.startswith("\t"):
             out[cur].append(line.strip())

@@ -85,7 +85,7 @@ OPERAND_CLASS = {
     "m48": "s[0:1]", "lhi": "s[0:1]",
     "G": "s0", "GI": "s0", "GE": "s0", "k80": "s0", "end": "s0", "dlo": "s0", "dhi": "s0", "ek": "s0", "ek2": "s0",
     "m": "s0", "gimask8": "s0", "gomask8": "s0", "gimask16": "s0", "gomask16": "s0", "crv0": "s0", "bpbase": "s0",
-    "fail": "s0", "slow": "s0",
+    "fail": "s0", "slow": "s0", "ekp": "s0", "ek2p": "s0",
 }
 _SIZE_CACHE = {}
 _PROMOTABLE = ("v_mov_b32", "v_add_u32", "v_sub_u32", "v_subrev_u32", "v_xor_b32", "v_max_i32", "v_max_u32",
@@ -416,11 +416,12 @@ RR = 512                 # LDS ring rows per in-workgroup link (sw_flow3.hip F3R
 RING = dict(H="v42", HGO="v43", HB="v44", HGOB="v45", TA="v46", TB="v47", PA="v48", PB="v49", M="v50")
 
 
-def ring_granule(a):
+def ring_granule(a, key="%[ek]", cp="sc1"):
     """Publish lanes 32..63 of IO (the 32 newest outflow rows, row v107) as 8-B granules
-    at their ring slots, rows outside [0, m) dropped."""
+    at their ring slots, rows outside [0, m) dropped.  A slab's outflow to the next GPU
+    (OUT = peer): key %[ekp], system scope (sc0 sc1)."""
     a("v_mov_b32 v96, v40")
-    a("v_xor_b32 v97, %[ek], v40")
+    a(f"v_xor_b32 v97, {key}, v40")
     a("v_xor_b32 v97, v97, v100")
     a("v_cmp_gt_u32_e64 s[50:51], %[m], v107")          # 0 <= row < m (unsigned)
     a("s_and_b64 s[50:51], s[50:51], %[lhi]")
@@ -429,10 +430,10 @@ def ring_granule(a):
     a("v_and_b32 v98, %[gomask8], v98")
     a("v_add_u32 v100, 0x400, v100")
     a("v_add_u32 v107, 32, v107")
-    a("buffer_store_dwordx2 v[96:97], v99, %[gors], 0 offen sc1")
+    a(f"buffer_store_dwordx2 v[96:97], v99, %[gors], 0 offen {cp}")
 
 
-def ring_gin_check(a, C=64):
+def ring_gin_check(a, C=64, key="%[ek]"):
     """s[58:59] = live lanes (lane < C, row k0 + lane < m); s[50:51] = live lanes whose granule fails."""
     a("s_sub_i32 s54, %[m], s40")
     if C < 64:
@@ -440,7 +441,7 @@ def ring_gin_check(a, C=64):
     a("v_cmp_gt_i32_e64 s[58:59], s54, %[lane]")
     a("v_xor_b32 v103, v84, v85")
     a("v_xor_b32 v103, v103, v102")
-    a("v_cmp_ne_u32_e64 s[56:57], %[ek], v103")
+    a(f"v_cmp_ne_u32_e64 s[56:57], {key}, v103")
     a("s_and_b64 s[50:51], s[58:59], s[56:57]")
     a("s_cmp_lg_u64 s[50:51], 0")
 
@@ -457,7 +458,11 @@ def gen_role_ring(IN, OUT_, C=64, hl=False):
     L = []
     a = L.append
     lds_in, lds_out = IN == "lds", OUT_ == "lds"
-    gin, gout = IN == "gran", OUT_ == "gran"
+    # granule inflow / outflow: ring edges (gran, device scope) or a column slab's edge to / from
+    # another GPU (peer: system scope sc0 sc1, the slab key %[ekp]; linear edges, no back-pressure)
+    gin, gout = IN in ("gran", "peer"), OUT_ in ("gran", "peer")
+    kin, cin = ("%[ekp]", "sc0 sc1") if IN == "peer" else ("%[ek]", "sc1")
+    kout, cout = ("%[ekp]", "sc0 sc1") if OUT_ == "peer" else ("%[ek]", "sc1")
     assert not hl or C == 64
     H = C // 2 if hl else C
     ncr = C // 16                                      # 16-B code reads per chunk
@@ -495,7 +500,7 @@ def gen_role_ring(IN, OUT_, C=64, hl=False):
     if gin:
         a("v_mov_b32 v101, %[gioff]")
         a("v_mov_b32 v102, %[gipos]")
-        a("buffer_load_dwordx2 v[84:85], v101, %[girs], 0 offen sc1")
+        a(f"buffer_load_dwordx2 v[84:85], v101, %[girs], 0 offen {cin}")
     for q in range(ncr):
         a(f"ds_read_b128 v[{52 + 4 * q}:{55 + 4 * q}], %[c0]" + (f" offset:{16 * q}" if q else ""))
     a("s_waitcnt vmcnt(0) lgkmcnt(0)")
@@ -528,7 +533,7 @@ def gen_role_ring(IN, OUT_, C=64, hl=False):
             a("s_cmp_lt_i32 s54, 0")
             a(f"s_cbranch_scc1 L_bpg{p}_%=")
             a(f"L_bpgr{p}_%=:")
-            ring_granule(a)
+            ring_granule(a, kout, cout)
         # 2. this chunk's inflow words / rows (LDS)
         if lds_in:
             a("ds_read_b32 v86, %[pin]")
@@ -540,7 +545,7 @@ def gen_role_ring(IN, OUT_, C=64, hl=False):
         stores_after = (2 if C == 64 else 1) * gout + (1 if gin and p == 0 else 0)
         a(f"s_waitcnt vmcnt({stores_after})")
         if gin:
-            ring_gin_check(a, C)
+            ring_gin_check(a, C, kin)
             a(f"s_cbranch_scc1 L_gin{p}_%=")
             a(f"L_ginr{p}_%=:")
             a("v_cndmask_b32_e64 v40, %[ng], v84, s[58:59]")
@@ -571,7 +576,7 @@ def gen_role_ring(IN, OUT_, C=64, hl=False):
             a(f"v_add_u32 v101, {C * 8:#x}, v101")
             a("v_and_b32 v101, %[gimask8], v101")
             a(f"v_add_u32 v102, {C << 5:#x}, v102")
-            a("buffer_load_dwordx2 v[84:85], v101, %[girs], 0 offen sc1")
+            a(f"buffer_load_dwordx2 v[84:85], v101, %[girs], 0 offen {cin}")
             if p == 1:   # every other chunk: rows consumed (for the producer's back-pressure)
                 a(f"s_add_u32 s54, s40, {C}")
                 a("s_min_i32 s54, s54, %[m]")
@@ -630,7 +635,7 @@ def gen_role_ring(IN, OUT_, C=64, hl=False):
                 io, l0 = ("v40", "v41") if b % 2 == 0 else ("v41", "v40")
                 step(a, io, l0, b, RING)
             if gout and C == 64 and u == 7:
-                ring_granule(a)
+                ring_granule(a, kout, cout)
         # 9. on to the next chunk
         a(f"s_add_i32 s40, s40, {C}")
         if lds_out:
@@ -659,7 +664,7 @@ def gen_role_ring(IN, OUT_, C=64, hl=False):
         a("s_cmp_lt_i32 s54, 0")
         a("s_cbranch_scc1 L_bpgx_%=")
         a("L_bpgxr_%=:")
-        ring_granule(a)
+        ring_granule(a, kout, cout)
     if gin:   # every row consumed
         a("s_add_u32 s54, %[m], %[crv0]")
         a("v_mov_b32 v104, s54")
@@ -684,7 +689,7 @@ def gen_role_ring(IN, OUT_, C=64, hl=False):
             slow_bp_hbm(a, lab, res)
     if gin:
         for p in (0, 1):
-            slow_gin(a, f"L_gin{p}_%=", f"L_ginr{p}_%=", C)
+            slow_gin(a, f"L_gin{p}_%=", f"L_ginr{p}_%=", C, kin, cin)
     a("L_done_%=:")
     return L
 
@@ -721,17 +726,17 @@ def slow_bp_hbm(a, label, resume):
     a(f"s_branch {resume}")
 
 
-def slow_gin(a, label, resume, C=64):
+def slow_gin(a, label, resume, C=64, key="%[ek]", cp="sc1"):
     """The chunk's inflow granules are not all published yet: re-load and re-check."""
     a(f"{label}:")
     a("s_add_u32 s46, s46, 1")
     a("s_cmp_lg_u32 s45, 0")
     a(f"s_cbranch_scc1 {resume}")
     a(f"{label}_w:")
-    a("buffer_load_dwordx2 v[84:85], v101, %[girs], 0 offen sc1")
+    a(f"buffer_load_dwordx2 v[84:85], v101, %[girs], 0 offen {cp}")
     a("s_memrealtime s[48:49]")
     a("s_waitcnt vmcnt(0) lgkmcnt(0)")
-    ring_gin_check(a, C)
+    ring_gin_check(a, C, key)
     a(f"s_cbranch_scc0 {resume}")
     slow_timeout(a, label)
     a(f"{label}_x:")
@@ -740,6 +745,10 @@ def slow_gin(a, label, resume, C=64):
 
 
 ROLES_IN_RING = ("none", "lds", "gran")
+# the extra roles of a column slab's kernel (C = 64): its first strip takes the previous GPU's
+# edge (IN = peer), its last strip hands its edge to the next GPU (OUT = peer)
+ROLES_SLAB = (("peer", "lds"), ("peer", "peer"), ("peer", "none"), ("gran", "peer"), ("lds", "peer"),
+              ("none", "peer"))
 CLOBBERS_RING = ['"v%d"' % r for r in range(40, 108) if r != 51] + \
     ['"s%d"' % r for r in range(40, 60) if r not in (47,)] + ['"scc"', '"vcc"', '"memory"']
 
@@ -749,8 +758,10 @@ def emit_ring():
            "// (sw_flow3.hip sw_flow3r_kernel): one inline-asm block per (chunk rows C, half-chunk LDS links HL, strip role), R = %d." % RR,
            "// Operands: see F3RLoop in sw_flow3.hip; fixed registers: tools/gen_flow3.py.",
            "#pragma once", ""]
-    for C, hl in ((64, 0), (32, 0), (64, 1)):
-        for IN, OUT_ in [(i, o) for i in ROLES_IN_RING for o in ROLES_OUT]:
+    combos = [(C, hl, i, o) for C, hl in ((64, 0), (32, 0), (64, 1)) for i in ROLES_IN_RING for o in ROLES_OUT]
+    combos += [(64, 0, i, o) for i, o in ROLES_SLAB]
+    for C, hl, IN, OUT_ in combos:
+        if True:
             body = gen_role_ring(IN, OUT_, C, bool(hl))
             out.append("template <> __device__ __forceinline__ F3Res f3r_loop<%d, %d, F3_%s, F3_%s>(const F3RLoop& x) {"
                        % (C, hl, IN.upper(), OUT_.upper()))
@@ -769,7 +780,7 @@ def emit_ring():
             out.append('          [ek] "s"(x.ek), [cross] "s"(x.cross), [crv0] "s"(x.crv0), [croff] "v"(x.croff),')
             out.append('          [gors] "s"(x.gors), [gooff] "v"(x.gooff), [gopos] "v"(x.gopos), [gomask8] "s"(x.gomask8),')
             out.append('          [gorow] "v"(x.gorow), [lhi] "s"(x.lhi), [bpr] "s"(x.bpr), [bpbase] "s"(x.bpbase),')
-            out.append('          [lmid] "v"(x.lmid)')
+            out.append('          [lmid] "v"(x.lmid), [ekp] "s"(x.ekp)')
             out.append("        : " + ", ".join(CLOBBERS_RING) + ");")
             out.append("    return r;")
             out.append("}")
@@ -1077,14 +1088,14 @@ def step_aff2(a, b, even):
     a("v_max3_i32 v57, v57, v51, v52")          # M
 
 
-def ring_granule_aff(a):
+def ring_granule_aff(a, key="%[ek]", key2="%[ek2]", cp="sc1"):
     """Publish lanes 32..63 of the I/O pair (the 32 newest outflow rows, row v117) as 16-B
-    granules at their ring slots, rows outside [0, m) dropped."""
+    granules at their ring slots, rows outside [0, m) dropped (peer: slab keys, system scope)."""
     a("v_mov_b32 v104, v40")
-    a("v_xor_b32 v105, %[ek], v40")
+    a(f"v_xor_b32 v105, {key}, v40")
     a("v_xor_b32 v105, v105, v110")
     a("v_mov_b32 v106, v41")
-    a("v_xor_b32 v107, %[ek2], v41")
+    a(f"v_xor_b32 v107, {key2}, v41")
     a("v_xor_b32 v107, v107, v110")
     a("v_cmp_gt_u32_e64 s[50:51], %[m], v117")
     a("s_and_b64 s[50:51], s[50:51], %[lhi]")
@@ -1093,20 +1104,20 @@ def ring_granule_aff(a):
     a("v_and_b32 v108, %[gomask16], v108")
     a("v_add_u32 v110, 0x400, v110")
     a("v_add_u32 v117, 32, v117")
-    a("buffer_store_dwordx4 v[104:107], v109, %[gors], 0 offen sc1")
+    a(f"buffer_store_dwordx4 v[104:107], v109, %[gors], 0 offen {cp}")
 
 
-def ring_gin_check_aff(a):
+def ring_gin_check_aff(a, key="%[ek]", key2="%[ek2]"):
     """s[58:59] = live lanes (row k0 + lane < m); s[50:51] = live lanes whose granule fails
     either half's check."""
     a("s_sub_i32 s54, %[m], s40")
     a("v_cmp_gt_i32_e64 s[58:59], s54, %[lane]")
     a("v_xor_b32 v113, v90, v91")
     a("v_xor_b32 v113, v113, v112")
-    a("v_cmp_ne_u32_e64 s[56:57], %[ek], v113")
+    a(f"v_cmp_ne_u32_e64 s[56:57], {key}, v113")
     a("v_xor_b32 v113, v92, v93")
     a("v_xor_b32 v113, v113, v112")
-    a("v_cmp_ne_u32_e64 vcc, %[ek2], v113")
+    a(f"v_cmp_ne_u32_e64 vcc, {key2}, v113")
     a("s_or_b64 s[56:57], s[56:57], vcc")
     a("s_and_b64 s[50:51], s[58:59], s[56:57]")
     a("s_cmp_lg_u64 s[50:51], 0")
@@ -1118,7 +1129,9 @@ def gen_role_ring_aff(IN, OUT_):
     L = []
     a = L.append
     lds_in, lds_out = IN == "lds", OUT_ == "lds"
-    gin, gout = IN == "gran", OUT_ == "gran"
+    gin, gout = IN in ("gran", "peer"), OUT_ in ("gran", "peer")
+    kin = ("%[ekp]", "%[ek2p]", "sc0 sc1") if IN == "peer" else ("%[ek]", "%[ek2]", "sc1")
+    kout = ("%[ekp]", "%[ek2p]", "sc0 sc1") if OUT_ == "peer" else ("%[ek]", "%[ek2]", "sc1")
     ncr = C // 16
     a("s_nop 4")
     a("s_waitcnt vmcnt(0) lgkmcnt(0)")
@@ -1152,7 +1165,7 @@ def gen_role_ring_aff(IN, OUT_):
     if gin:
         a("v_mov_b32 v111, %[gioff]")
         a("v_mov_b32 v112, %[gipos]")
-        a("buffer_load_dwordx4 v[90:93], v111, %[girs], 0 offen sc1")
+        a(f"buffer_load_dwordx4 v[90:93], v111, %[girs], 0 offen {kin[2]}")
     for q in range(ncr):
         a(f"ds_read_b128 v[{58 + 4 * q}:{61 + 4 * q}], %[c0]" + (f" offset:{16 * q}" if q else ""))
     a("s_waitcnt vmcnt(0) lgkmcnt(0)")
@@ -1178,7 +1191,7 @@ def gen_role_ring_aff(IN, OUT_):
             a("s_cmp_lt_i32 s54, 0")
             a(f"s_cbranch_scc1 L_bpg{p}_%=")
             a(f"L_bpgr{p}_%=:")
-            ring_granule_aff(a)
+            ring_granule_aff(a, *kout)
         if lds_in:
             a("ds_read_b32 v94, %[pin]")
             a("ds_read_b64 v[90:91], v96")
@@ -1186,7 +1199,7 @@ def gen_role_ring_aff(IN, OUT_):
         stores_after = 2 * gout + (1 if gin and p == 0 else 0)
         a(f"s_waitcnt vmcnt({stores_after})")
         if gin:
-            ring_gin_check_aff(a)
+            ring_gin_check_aff(a, kin[0], kin[1])
             a(f"s_cbranch_scc1 L_gin{p}_%=")
             a(f"L_ginr{p}_%=:")
             a("v_cndmask_b32_e64 v40, %[ng], v90, s[58:59]")
@@ -1216,7 +1229,7 @@ def gen_role_ring_aff(IN, OUT_):
             a(f"v_add_u32 v111, {C * 16:#x}, v111")
             a("v_and_b32 v111, %[gimask16], v111")
             a(f"v_add_u32 v112, {C << 5:#x}, v112")
-            a("buffer_load_dwordx4 v[90:93], v111, %[girs], 0 offen sc1")
+            a(f"buffer_load_dwordx4 v[90:93], v111, %[girs], 0 offen {kin[2]}")
             if p == 1:
                 a(f"s_add_u32 s54, s40, {C}")
                 a("s_min_i32 s54, s54, %[m]")
@@ -1249,7 +1262,7 @@ def gen_role_ring_aff(IN, OUT_):
             for b in range(4):
                 step_aff2(a, b, b % 2 == 0)
             if gout and u == 7:
-                ring_granule_aff(a)
+                ring_granule_aff(a, *kout)
         a(f"s_add_i32 s40, s40, {C}")
         if lds_out:
             a(f"s_add_u32 s41, s41, {SZA * C:#x}")
@@ -1276,7 +1289,7 @@ def gen_role_ring_aff(IN, OUT_):
         a("s_cmp_lt_i32 s54, 0")
         a("s_cbranch_scc1 L_bpgx_%=")
         a("L_bpgxr_%=:")
-        ring_granule_aff(a)
+        ring_granule_aff(a, *kout)
     if gin:
         a("s_add_u32 s54, %[m], %[crv0]")
         a("v_mov_b32 v114, s54")
@@ -1297,7 +1310,7 @@ def gen_role_ring_aff(IN, OUT_):
             slow_bp_hbm_aff(a, lab, res)
     if gin:
         for p in (0, 1):
-            slow_gin_aff(a, f"L_gin{p}_%=", f"L_ginr{p}_%=")
+            slow_gin_aff(a, f"L_gin{p}_%=", f"L_ginr{p}_%=", *kin)
     a("L_done_%=:")
     return L
 
@@ -1322,16 +1335,16 @@ def slow_bp_hbm_aff(a, label, resume):
     a(f"s_branch {resume}")
 
 
-def slow_gin_aff(a, label, resume):
+def slow_gin_aff(a, label, resume, key="%[ek]", key2="%[ek2]", cp="sc1"):
     a(f"{label}:")
     a("s_add_u32 s46, s46, 1")
     a("s_cmp_lg_u32 s45, 0")
     a(f"s_cbranch_scc1 {resume}")
     a(f"{label}_w:")
-    a("buffer_load_dwordx4 v[90:93], v111, %[girs], 0 offen sc1")
+    a(f"buffer_load_dwordx4 v[90:93], v111, %[girs], 0 offen {cp}")
     a("s_memrealtime s[48:49]")
     a("s_waitcnt vmcnt(0) lgkmcnt(0)")
-    ring_gin_check_aff(a)
+    ring_gin_check_aff(a, key, key2)
     a(f"s_cbranch_scc0 {resume}")
     slow_timeout(a, label)
     a(f"{label}_x:")
@@ -1349,7 +1362,7 @@ def emit_ring_aff():
            "// (sw_flow3.hip sw_flow3ra_kernel): one inline-asm block per strip role, C = 64, R = %d rows of 8-B slots." % RR,
            "// Operands: see F3RALoop in sw_flow3.hip; fixed registers: tools/gen_flow3.py (gen_role_ring_aff).",
            "#pragma once", ""]
-    for IN, OUT_ in [(i, o) for i in ROLES_IN_RING for o in ROLES_OUT]:
+    for IN, OUT_ in [(i, o) for i in ROLES_IN_RING for o in ROLES_OUT] + list(ROLES_SLAB):
         body = gen_role_ring_aff(IN, OUT_)
         out.append("template <> __device__ __forceinline__ F3Res f3ra_loop<F3_%s, F3_%s>(const F3RALoop& x) {"
                    % (IN.upper(), OUT_.upper()))
@@ -1367,7 +1380,8 @@ def emit_ring_aff():
         out.append('          [girs] "s"(x.girs), [gioff] "v"(x.gioff), [gipos] "v"(x.gipos), [gimask16] "s"(x.gimask16),')
         out.append('          [ek] "s"(x.ek), [ek2] "s"(x.ek2), [cross] "s"(x.cross), [crv0] "s"(x.crv0), [croff] "v"(x.croff),')
         out.append('          [gors] "s"(x.gors), [gooff] "v"(x.gooff), [gopos] "v"(x.gopos), [gomask16] "s"(x.gomask16),')
-        out.append('          [gorow] "v"(x.gorow), [lhi] "s"(x.lhi), [bpr] "s"(x.bpr), [bpbase] "s"(x.bpbase)')
+        out.append('          [gorow] "v"(x.gorow), [lhi] "s"(x.lhi), [bpr] "s"(x.bpr), [bpbase] "s"(x.bpbase),')
+        out.append('          [ekp] "s"(x.ekp), [ek2p] "s"(x.ek2p)')
         out.append("        : " + ", ".join(CLOBBERS_RING_AFF) + ");")
         out.append("    return r;")
         out.append("}")
