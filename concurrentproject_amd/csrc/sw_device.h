@@ -23,6 +23,25 @@ constexpr int SENT_BYTE = 0x100;       // never equal to a column byte
 constexpr int DEAD_COL_BYTE = 0x200;   // dead (past-the-end) column value, byte mode
 constexpr int DEAD = 1 << 29;          // t offset that keeps dead columns out of the max
 
+// The same for a spin loop that keeps its own start time: n counts the polls (one counter per
+// strip pass, shared by its loops).
+__device__ __forceinline__ bool spin_expired(int& n, long long t0, long long ticks) {
+    return ((++n & 63) == 0) && ((long long)__builtin_amdgcn_s_memrealtime() - t0 > ticks);
+}
+
+// Deadline of a spin loop.  The clock (s_memrealtime) is an SMEM round trip far slower than
+// the LDS or L2 poll it guards, so it is read only every 64th poll: read every poll, it set
+// the pace of every late hand-off (r05: a column slab's in-workgroup hops 9.6 us).
+struct SpinDeadline {
+    long long t0;
+    long long ticks;
+    int n;
+    __device__ SpinDeadline(long long start, long long timeout) : t0(start), ticks(timeout), n(0) {}
+    __device__ __forceinline__ bool expired() {
+        return ((++n & 63) == 0) && ((long long)__builtin_amdgcn_s_memrealtime() - t0 > ticks);
+    }
+};
+
 __device__ __forceinline__ int dpp_shr1(int old, int src) {
     return __builtin_amdgcn_update_dpp(old, src, DPP_WAVE_SHR1, 0xF, 0xF, false);
 }
@@ -178,14 +197,14 @@ __device__ __noinline__ AwaitRes await_slow(__amdgpu_buffer_rsrc_t rsrc, unsigne
                                             const long long timeout_ticks, Ctrl* ctrl, const int strip,
                                             const int lane) {
     const Edge e{rsrc, pos0, mask, epoch};
-    const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+    SpinDeadline dl((long long)__builtin_amdgcn_s_memrealtime(), timeout_ticks);
     bool ok = !need || granule_ok(g, e, row);
     for (;;) {
         __builtin_amdgcn_s_sleep(1);
         if (!ok) g = __builtin_amdgcn_raw_buffer_load_b128(e.rsrc, edge_off(e, row), 0, AUX);
         ok = !need || granule_ok(g, e, row);
         if (__all(ok)) return AwaitRes{g, 0};
-        if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > timeout_ticks) {
+        if (dl.expired()) {
             if (lane == 0) {
                 atomicOr(&ctrl->error, ERR_TIMEOUT);
                 atomicMax(&ctrl->err_item, (unsigned)strip);

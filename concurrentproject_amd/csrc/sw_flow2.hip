@@ -286,6 +286,7 @@ __global__ void __launch_bounds__(f2_threads<STREAM>()) sw_flow2_kernel(KParams 
             if (group > 0 && 4 * group < pd.strips) {
                 const Edge le = group_edge(kp, pd, group - 1, (pd.strips + 3) / 4);
                 const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+                [[maybe_unused]] int spin_n = 0;   // polls (spin_expired)
                 int2* const lring = ring[4];
                 int* const lprod = lane == 0 ? &prod[4] : &psink[4][lane];
                 int base = 0, sent = 0, cseen = 0;
@@ -326,9 +327,9 @@ __global__ void __launch_bounds__(f2_threads<STREAM>()) sw_flow2_kernel(KParams 
                         cseen = __builtin_amdgcn_readfirstlane(lds_load(&cons[0]));
                         if (cseen >= floor_rows) break;
                         __builtin_amdgcn_s_sleep(SW_SPIN_SLEEP);
-                        if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > kp.timeout_ticks) break;
+                        if (spin_expired(spin_n, t0, kp.timeout_ticks)) break;
                     }
-                    if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > kp.timeout_ticks) {
+                    if (spin_expired(spin_n, t0, kp.timeout_ticks)) {
                         lfail = true;
                         break;
                     }
@@ -395,6 +396,7 @@ __global__ void __launch_bounds__(f2_threads<STREAM>()) sw_flow2_kernel(KParams 
             const __amdgpu_buffer_rsrc_t cons_rsrc = __builtin_amdgcn_make_buffer_rsrc(cons_live ? cons_in : nullptr, 0,
                                                                                         cons_live ? 4 : 0, RSRC_FLAGS);
             const long long t_start = (long long)__builtin_amdgcn_s_memrealtime();
+            [[maybe_unused]] int spin_n = 0;   // polls (spin_expired)
             bool failed = false;
             long long t_first = t_start;
             int nslow = 0;   // chunks whose inflow took the slow path (trace only)
@@ -485,7 +487,7 @@ __global__ void __launch_bounds__(f2_threads<STREAM>()) sw_flow2_kernel(KParams 
                                 __builtin_amdgcn_s_sleep(SW_SPIN_SLEEP);
                                 bp_seen = __builtin_amdgcn_readfirstlane(
                                     __hip_atomic_load(bp_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-                                if ((long long)__builtin_amdgcn_s_memrealtime() - t_start > kp.timeout_ticks) {
+                                if (spin_expired(spin_n, t_start, kp.timeout_ticks)) {
                                     failed = true;
                                     if (fail_bp < 0) fail_bp = k0;
                                     break;
@@ -518,7 +520,7 @@ __global__ void __launch_bounds__(f2_threads<STREAM>()) sw_flow2_kernel(KParams 
                             while (cons_seen < floor_rows) {
                                 __builtin_amdgcn_s_sleep(SW_SPIN_SLEEP);
                                 cons_seen = __builtin_amdgcn_readfirstlane(lds_load(cons_next));
-                                if ((long long)__builtin_amdgcn_s_memrealtime() - t_start > kp.timeout_ticks) {
+                                if (spin_expired(spin_n, t_start, kp.timeout_ticks)) {
                                     failed = true;
                                     break;
                                 }
@@ -589,7 +591,7 @@ __global__ void __launch_bounds__(f2_threads<STREAM>()) sw_flow2_kernel(KParams 
                                 while (avail < need) {
                                     __builtin_amdgcn_s_sleep(SW_SPIN_SLEEP);
                                     avail = __builtin_amdgcn_readfirstlane(lds_load(&prod[in_w]));
-                                    if ((long long)__builtin_amdgcn_s_memrealtime() - t_start > kp.timeout_ticks) {
+                                    if (spin_expired(spin_n, t_start, kp.timeout_ticks)) {
                                         failed = true;
                                         break;
                                     }
@@ -611,7 +613,7 @@ __global__ void __launch_bounds__(f2_threads<STREAM>()) sw_flow2_kernel(KParams 
                                     avail = lds_load(&prod[in_w]);
                                     compiler_fence();
                                     v = in_slot(k0 + (lane & (HL - 1)));
-                                    if ((long long)__builtin_amdgcn_s_memrealtime() - t_start > kp.timeout_ticks) {
+                                    if (spin_expired(spin_n, t_start, kp.timeout_ticks)) {
                                         failed = true;
                                         break;
                                     }
@@ -688,7 +690,7 @@ __global__ void __launch_bounds__(f2_threads<STREAM>()) sw_flow2_kernel(KParams 
                                         h_avail = lds_load(&prod[in_w]);
                                         compiler_fence();
                                         h_v = in_ring[(pb_in + k0 + HL + (lane & (HL - 1))) & (R - 1)];
-                                        if ((long long)__builtin_amdgcn_s_memrealtime() - t_start > kp.timeout_ticks) {
+                                        if (spin_expired(spin_n, t_start, kp.timeout_ticks)) {
                                             failed = true;
                                             break;
                                         }

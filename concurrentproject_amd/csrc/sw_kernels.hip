@@ -496,6 +496,7 @@ __global__ void __launch_bounds__(256) sw_flow_kernel(KParams kp) {
         const int nloc = (m + SW - 1 + C - 1) / C;
         bool failed = false;
         const long long t_start = (long long)__builtin_amdgcn_s_memrealtime();
+        [[maybe_unused]] int spin_n = 0;   // polls (spin_expired)
         long long t_first = t_start;
         int spins = 0;
         unsigned long long cyc_pro = 0, cyc_run = 0, cyc_epi = 0;
@@ -551,7 +552,7 @@ __global__ void __launch_bounds__(256) sw_flow_kernel(KParams kp) {
                             avail = lds_load(&prod[wave - 1]);
                             compiler_fence();
                             v = ring[wave - 1][row & (R - 1)];
-                            if ((long long)__builtin_amdgcn_s_memrealtime() - t_start > kp.timeout_ticks) {
+                            if (spin_expired(spin_n, t_start, kp.timeout_ticks)) {
                                 failed = true;   // reported after the strip: no global op in the loop
                                 break;
                             }
@@ -586,7 +587,7 @@ __global__ void __launch_bounds__(256) sw_flow_kernel(KParams kp) {
                             while (cons_seen < floor_rows) {
                                 __builtin_amdgcn_s_sleep(SW_SPIN_SLEEP);
                                 cons_seen = __builtin_amdgcn_readfirstlane(lds_load(&cons[wave + 1]));
-                                if ((long long)__builtin_amdgcn_s_memrealtime() - t_start > kp.timeout_ticks) {
+                                if (spin_expired(spin_n, t_start, kp.timeout_ticks)) {
                                     failed = true;
                                     break;
                                 }
@@ -1113,7 +1114,7 @@ __device__ void strip_pass_duo_lds(const KParams& kp, const DuoDesc& d, const in
                                    const bool has_in, const DuoLink<LIN> in, const bool has_out,
                                    const DuoLink<LIN> out, int* const prod_out, int* const cons_out,
                                    DuoSlot<LIN>* const sink, unsigned* const tab, const bool build,
-                                   int* const ready_out, const int ready_val) {
+                                   int* const ready_out, const int ready_val, const int prio_par) {
     constexpr int SW = 64 * W;
     static_assert(C == 64, "the LDS links move one row per lane and chunk");
     const int m = d.m_pad;
@@ -1146,11 +1147,19 @@ __device__ void strip_pass_duo_lds(const KParams& kp, const DuoDesc& d, const in
     if constexpr (TAB) S.setup(kp, d, strip, lane, tab);
     else S.setup(kp, d, strip, lane);
     const long long t_start = (long long)__builtin_amdgcn_s_memrealtime();
+    [[maybe_unused]] int spin_n = 0;   // polls (spin_expired)
     bool failed = false;
     int cons_seen = 0;
     for (int c = 0; c < nchunks; ++c) {
         const int k0 = c * C;
         const unsigned raw0 = raw0_nxt, raw1 = raw1_nxt;
+        // kp.duo_prio: the CU's two workgroups (prio_par 0 / 1) take turns at issue priority, so
+        // neither runs alone on its SIMDs at the end (old-wave-first arbitration otherwise lets
+        // the first one finish far ahead: wave end times at ~3.2 and ~6.4 ms on C3)
+        if (prio_par >= 0) {
+            if ((((unsigned)c >> (kp.duo_prio - 1)) ^ (unsigned)prio_par) & 1u) __builtin_amdgcn_s_setprio(2);
+            else __builtin_amdgcn_s_setprio(0);
+        }
         if constexpr (TAB) {
             if (build) {   // table rows k0 + 128 .. k0 + 191 (bytes loaded a chunk ago), bytes of the next 64
                 tab[DUO_TAB_OFF + k0 + 128 + lane] = codes_duo(raw0, raw1, k0 + 128, lane, C, d);
@@ -1176,7 +1185,7 @@ __device__ void strip_pass_duo_lds(const KParams& kp, const DuoDesc& d, const in
                     avail = lds_load(in.prod);
                     compiler_fence();
                     v = *src;
-                    if ((long long)__builtin_amdgcn_s_memrealtime() - t_start > kp.timeout_ticks) {
+                    if (spin_expired(spin_n, t_start, kp.timeout_ticks)) {
                         failed = true;
                         break;
                     }
@@ -1211,7 +1220,7 @@ __device__ void strip_pass_duo_lds(const KParams& kp, const DuoDesc& d, const in
                     while (cons_seen < floor_pos) {
                         __builtin_amdgcn_s_sleep(1);
                         cons_seen = __builtin_amdgcn_readfirstlane(lds_load(out.cons));
-                        if ((long long)__builtin_amdgcn_s_memrealtime() - t_start > kp.timeout_ticks) {
+                        if (spin_expired(spin_n, t_start, kp.timeout_ticks)) {
                             failed = true;
                             break;
                         }
@@ -1293,6 +1302,13 @@ __global__ void __launch_bounds__(64 * DUO_WAVES) sw_duo_lds_kernel(KParams kp) 
         else if (roles > 0) wave = 3 - ((my_simd - (roles & 3)) & 3);
     }
     wave = __builtin_amdgcn_readfirstlane(wave);
+    // turn-taking parity (kp.duo_prio): the first workgroup on a CU 0, the second 1, else off
+    int prio_par = -1;
+    if (kp.ring_cons != nullptr && kp.duo_prio > 0) {
+        const int roles = s_roles;
+        prio_par = roles == 0 ? 0 : roles > 0 ? 1 : -1;
+    }
+    prio_par = __builtin_amdgcn_readfirstlane(prio_par);
     const unsigned wmask = (unsigned)kp.wrap_rows - 1u;
     // progress words: lane 0 writes the word, the others a sink (no exec-mask branch)
     int* const prod_out = lane == 0 ? &prod[wave] : &psink[wave][lane];
@@ -1303,6 +1319,7 @@ __global__ void __launch_bounds__(64 * DUO_WAVES) sw_duo_lds_kernel(KParams kp) 
     int dseq = 0;             // duos this workgroup has begun
     // tools/probe_duo_simd.py: where each wave runs (HW_ID: SIMD, CU, SE; XCC_ID) and when
     const long long t_begin = (long long)__builtin_amdgcn_s_memrealtime();
+    [[maybe_unused]] int spin_n = 0;   // polls (spin_expired)
     bool failed = false;
     for (int di = blockIdx.x; di < kp.npairs; di += gridDim.x, ++dseq) {
         const DuoDesc d = load_duo(kp, di);
@@ -1315,7 +1332,7 @@ __global__ void __launch_bounds__(64 * DUO_WAVES) sw_duo_lds_kernel(KParams kp) 
                                               : lds_load(&tabready) >= dseq + 1;
                     if (__builtin_amdgcn_readfirstlane((int)ok)) break;
                     __builtin_amdgcn_s_sleep(1);
-                    if ((long long)__builtin_amdgcn_s_memrealtime() - t_begin > kp.timeout_ticks) {
+                    if (spin_expired(spin_n, t_begin, kp.timeout_ticks)) {
                         failed = true;
                         break;
                     }
@@ -1332,7 +1349,7 @@ __global__ void __launch_bounds__(64 * DUO_WAVES) sw_duo_lds_kernel(KParams kp) 
                                        wave < 3 ? base : 0, base, nullptr, wave < 3 ? &cons[wave + 1] : nullptr};
                 strip_pass_duo_lds<W, C, M3, LIN, TAB>(kp, d, strip, lane, strip > 0, in, strip + 1 < d.strips, out,
                                                        prod_out, cons_out, sink[wave], tab, strip == 0, ready_out,
-                                                       dseq + 1);
+                                                       dseq + 1, prio_par);
             }
             // done with every position before the next round, read or not: a producer's back-pressure
             // must not wait on a consumer that skipped rounds (idle waves of a duo's last round) --

@@ -43,7 +43,9 @@ OUT = os.path.join(ROOT, "concurrentproject_amd", "csrc", "sw_flow3_loops.inc")
 
 ROLES_IN = ("none", "lds")
 MID_AHEAD = int(os.environ.get("F3_MIDAHEAD", "1"))
-LOOP_PAD = int(os.environ.get("F3_LOOP_PAD", "0"))   # 4-B s_nop 0 between the 64-B boundary and the loop (A/B)   # 4-step groups the mid-chunk inflow read runs ahead
+LOOP_PAD = int(os.environ.get("F3_LOOP_PAD", "0"))
+RING_ALIGN = int(os.environ.get("F3_RING_ALIGN", "0"))   # A/B: align the ring loops too
+RING_NOPS = int(os.environ.get("F3_RING_NOPS", "0"))   # 4-B s_nop 0 between the 64-B boundary and the loop (A/B)   # 4-step groups the mid-chunk inflow read runs ahead
 ROLES_OUT = ("none", "lds", "gran")
 
 
@@ -118,9 +120,10 @@ def _sizes(lines):
             for l in lines]
 
 
-def align8(lines):
+def align8(lines, nops=True):
     """The loop of an asm block (from its 64-B aligned L_loop label to the loop's back branch)
-    with every 8-B instruction on an 8-B boundary (see above)."""
+    with every 8-B instruction on an 8-B boundary (see above); nops = False: re-encodings only
+    (an 8-B instruction after a run without a promotable one stays where it is)."""
     try:
         i0 = lines.index("L_loop_%=:")
         i1 = lines.index("s_cbranch_scc1 L_loop_%=")
@@ -134,9 +137,10 @@ def align8(lines):
             if cand is not None:
                 op, rest = out[cand].split(" ", 1)
                 out[cand] = op + "_e64 " + rest
-            else:
+                off += 4
+            elif nops:
                 out.append("s_nop 0")
-            off += 4
+                off += 4
             cand = None
         out.append(l)
         off += n
@@ -346,17 +350,11 @@ def slow_wait(a, label, resume, vreg, addr, sreg, reread=None, target="s40"):
     a(f"ds_read_b32 {vreg}, {addr}")
     if reread:
         a(reread)
-    a("s_memrealtime s[48:49]")
     a("s_waitcnt lgkmcnt(0)")
     a(f"v_readfirstlane_b32 {sreg}, {vreg}")
     a(f"s_cmp_ge_i32 {sreg}, {target}")
     a(f"s_cbranch_scc1 {resume}")
-    a("s_sub_u32 s48, s48, %[dlo]")
-    a("s_subb_u32 s49, s49, %[dhi]")
-    a("s_cmp_lt_i32 s49, 0")
-    a("s_cbranch_scc0 %s_x" % label)
-    a("s_sleep 1")
-    a(f"s_branch {label}_w")
+    slow_timeout(a, label)
     a(f"{label}_x:")
     a("s_mov_b32 s45, 1")
     a(f"s_branch {resume}")
@@ -695,11 +693,21 @@ def gen_role_ring(IN, OUT_, C=64, hl=False):
 
 
 def slow_timeout(a, label):
-    """s[48:49] = s_memrealtime (waited): on to {label}_w unless past the deadline, then fail."""
+    """The end of a slow-path poll: sleep and poll again ({label}_w); every 64th poll also reads
+    the clock and gives up past the deadline ({label}_x).  s_memrealtime is an SMEM round trip
+    much slower than an LDS poll: read every poll, it set the pace of every late hand-off (a
+    column slab's in-workgroup hops took 9.6 us, r05)."""
+    a("s_add_u32 s46, s46, 1")
+    a("s_and_b32 s48, s46, 63")
+    a("s_cmp_lg_u32 s48, 0")
+    a(f"s_cbranch_scc1 {label}_s")
+    a("s_memrealtime s[48:49]")
+    a("s_waitcnt lgkmcnt(0)")
     a("s_sub_u32 s48, s48, %[dlo]")
     a("s_subb_u32 s49, s49, %[dhi]")
     a("s_cmp_lt_i32 s49, 0")
     a("s_cbranch_scc0 %s_x" % label)
+    a(f"{label}_s:")
     a("s_sleep 1")
     a(f"s_branch {label}_w")
 
@@ -713,7 +721,6 @@ def slow_bp_hbm(a, label, resume):
     a(f"s_cbranch_scc1 {resume}")
     a(f"{label}_w:")
     a("buffer_load_dword v92, off, %[bpr], 0 sc1")
-    a("s_memrealtime s[48:49]")
     a("s_waitcnt vmcnt(0) lgkmcnt(0)")
     a("v_readfirstlane_b32 s52, v92")
     a("s_add_u32 s55, s40, %[bpbase]")
@@ -734,7 +741,6 @@ def slow_gin(a, label, resume, C=64, key="%[ek]", cp="sc1"):
     a(f"s_cbranch_scc1 {resume}")
     a(f"{label}_w:")
     a(f"buffer_load_dwordx2 v[84:85], v101, %[girs], 0 offen {cp}")
-    a("s_memrealtime s[48:49]")
     a("s_waitcnt vmcnt(0) lgkmcnt(0)")
     ring_gin_check(a, C, key)
     a(f"s_cbranch_scc0 {resume}")
@@ -762,7 +768,7 @@ def emit_ring():
     combos += [(64, 0, i, o) for i, o in ROLES_SLAB]
     for C, hl, IN, OUT_ in combos:
         if True:
-            body = gen_role_ring(IN, OUT_, C, bool(hl))
+            body = align8(gen_role_ring(IN, OUT_, C, bool(hl)), nops=RING_NOPS) if RING_ALIGN else gen_role_ring(IN, OUT_, C, bool(hl))
             out.append("template <> __device__ __forceinline__ F3Res f3r_loop<%d, %d, F3_%s, F3_%s>(const F3RLoop& x) {"
                        % (C, hl, IN.upper(), OUT_.upper()))
             out.append("    F3Res r;")
@@ -1322,7 +1328,6 @@ def slow_bp_hbm_aff(a, label, resume):
     a(f"s_cbranch_scc1 {resume}")
     a(f"{label}_w:")
     a("buffer_load_dword v100, off, %[bpr], 0 sc1")
-    a("s_memrealtime s[48:49]")
     a("s_waitcnt vmcnt(0) lgkmcnt(0)")
     a("v_readfirstlane_b32 s52, v100")
     a("s_add_u32 s55, s40, %[bpbase]")
@@ -1342,7 +1347,6 @@ def slow_gin_aff(a, label, resume, key="%[ek]", key2="%[ek2]", cp="sc1"):
     a(f"s_cbranch_scc1 {resume}")
     a(f"{label}_w:")
     a(f"buffer_load_dwordx4 v[90:93], v111, %[girs], 0 offen {cp}")
-    a("s_memrealtime s[48:49]")
     a("s_waitcnt vmcnt(0) lgkmcnt(0)")
     ring_gin_check_aff(a, key, key2)
     a(f"s_cbranch_scc0 {resume}")
@@ -1363,7 +1367,7 @@ def emit_ring_aff():
            "// Operands: see F3RALoop in sw_flow3.hip; fixed registers: tools/gen_flow3.py (gen_role_ring_aff).",
            "#pragma once", ""]
     for IN, OUT_ in [(i, o) for i in ROLES_IN_RING for o in ROLES_OUT] + list(ROLES_SLAB):
-        body = gen_role_ring_aff(IN, OUT_)
+        body = align8(gen_role_ring_aff(IN, OUT_), nops=RING_NOPS) if RING_ALIGN else gen_role_ring_aff(IN, OUT_)
         out.append("template <> __device__ __forceinline__ F3Res f3ra_loop<F3_%s, F3_%s>(const F3RALoop& x) {"
                    % (IN.upper(), OUT_.upper()))
         out.append("    F3Res r;")
