@@ -64,8 +64,10 @@ def test_ring_mode_matches_oracle(engine, oracle_mod):
                 strips = ((n - 2 + 125) // 126 if n > 128 else 1) if st["variant"] & 16 else (n - 1 + 62) // 63
                 groups = (strips + 3) // 4
                 assert st["mode"] == 5 and bool(st["variant"] & 4) == (groups > 1), st
-                # two columns per lane exactly when the linear-gap step runs (G_INIT == G_EXT)
-                assert bool(st["variant"] & 16) == (prm.gap_init == prm.gap_ext), st
+                # two columns per lane when the linear-gap step runs (G_INIT == G_EXT), and in ring
+                # mode for the affine step too (flow3's sw_flow3ra_kernel, variant bit 1024)
+                ring_aff = bool(st["variant"] & 4 and st["variant"] & 1024)
+                assert bool(st["variant"] & 16) == (prm.gap_init == prm.gap_ext or ring_aff), st
                 assert groups == 1 or st["variant"] & 2, st   # ring mode streams the row codes
             assert got == exp, (prm, blocks, rows)
 
