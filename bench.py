@@ -351,11 +351,19 @@ def c5_runs(sw, torch, gold, steps):
                         "kernel_ms_per_launch": round(k, 3), "steps": steps,
                         "parity": ("ok" if scores[0].item() == g["score"] else "MISMATCH") if g else "unchecked",
                         "score": scores[0].item(), **kernel_label(sw.last_stats()),
-                        "boundary_bytes": sw.last_stats()["boundary_bytes"]}
+                        "boundary_bytes": sw.last_stats()["boundary_bytes"],
+                        "roofline": roofline("slab" if key == "linear" else "slab_affine", N * N, k,
+                                             waves_per_simd=resident_waves_per_simd(sw.last_stats(), torch))}
         finally:
             sw.set_params(sw.Params(1, -1, 1, 1))
     out["workload"] = "C5 single pair N=2^20 (seed 1048576), resident in HBM"
     return out
+
+
+def affine_key(st):
+    """"_affine" when a single-pair launch ran the general affine step (its counter profile is
+    profiles/pmc_<workload>_affine.json, tools/pmc_summary.py c2a / c5a)."""
+    return "_affine" if st["mode"] == 5 and not st["variant"] & 8 else ""
 
 
 def flow2_strips(n, w2=False):
@@ -808,7 +816,7 @@ def main():
             "kernel_gcups": round(per_launch_cells / (avg_kern_ms * 1e-3) / 1e9, 3),
             "parity": parity,
             "host_api": host_api,
-            "roofline": roofline(workload if args.slab_of <= 1 else "slab_part", per_launch_cells, avg_kern_ms,
+            "roofline": roofline((workload if args.slab_of <= 1 else "slab_part") + affine_key(st), per_launch_cells, avg_kern_ms,
                                  step_ns, cfg["N"], cfg["N"], bool(st["variant"] & 16),
                                  waves_per_simd=None if workload == "pair" else resident_waves_per_simd(st, torch)),
         }

@@ -1,4 +1,2 @@
 set -e
-TRACE_OPTS="ring=1" timeout -k 10 120 python tools/trace_flow.py 131072 64 1 131040 5 2 > gpurun_out/trace_s17.txt 2>&1
-TRACE_OPTS="ring=1" timeout -k 10 120 python tools/trace_flow.py 262144 64 1 131040 5 2 > gpurun_out/trace_s18.txt 2>&1
-TRACE_OPTS="ring=1" timeout -k 10 120 python tools/trace_flow.py 1048576 64 1 131040 5 2 > gpurun_out/trace_s20.txt 2>&1
+bash tools/prof_round.sh c2 c3 c5 c5p8 c2a c5a

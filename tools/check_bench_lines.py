@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Check committed bench lines against the counter profiles they were computed from.
 
-    python tools/check_bench_lines.py [profiles/r04*_bench_*.json ...]
+    python tools/check_bench_lines.py [profiles/r05*_bench_*.json ...]
 
 For every bench JSON line (the top-level roofline and the nested batch_c3 / batch_c4
 rooflines) whose roofline names a profiles/pmc_*.json and carries its sha256
@@ -34,19 +34,24 @@ def lines_of(path):
 
 
 def rooflines(line):
-    """(label, roofline, kernel ms) of a bench line and its nested batch line."""
+    """(label, roofline, kernel ms, kernel_fn) of a bench line and its nested lines (the batched
+    config, the affine step, the C5 extras)."""
     if "roofline" in line and "kernel_ms_per_launch" in line:
-        yield "main", line["roofline"], line["kernel_ms_per_launch"]
-    for key in ("batch_c3", "batch_c4"):
+        yield "main", line["roofline"], line["kernel_ms_per_launch"], (line.get("config") or {}).get("kernel_fn")
+    for key in ("batch_c3", "batch_c4", "affine_step"):
         sub = line.get(key)
         if isinstance(sub, dict) and "roofline" in sub:
-            yield key, sub["roofline"], sub["kernel_ms_per_launch"]
+            yield key, sub["roofline"], sub["kernel_ms_per_launch"], sub.get("kernel_fn")
+    for key in ("linear", "affine"):
+        sub = (line.get("c5") or {}).get(key)
+        if isinstance(sub, dict) and "roofline" in sub:
+            yield "c5." + key, sub["roofline"], sub["kernel_ms_per_launch"], sub.get("kernel_fn")
 
 
 def check(path, strict):
     bad = []
     for line in lines_of(path):
-        for label, rf, kms in rooflines(line):
+        for label, rf, kms, fn in rooflines(line):
             src = rf.get("source") or ""
             if not src.startswith("profiles/pmc_"):
                 if strict:
@@ -62,6 +67,10 @@ def check(path, strict):
                     bad.append("%s %s: STALE (%s changed since the line was taken)" % (path, label, src))
                 continue
             prof = json.load(open(pmc))
+            # the kernel the line says it timed is the one the profile counted
+            if fn is not None and "::" + fn + "<" not in prof["kernel"] and "::" + fn + "(" not in prof["kernel"]:
+                bad.append("%s %s: config kernel_fn %s but %s profiles %s" % (path, label, fn, src, prof["kernel"]))
+                continue
             ach = prof["valu_insts_per_launch"] * 64 / (kms * 1e-3) / 1e12
             frac = ach / PEAK
             if rf.get("frac") is None or abs(rf["frac"] - frac) > 0.0005 * max(1.0, frac) + 1e-4 \
@@ -76,7 +85,7 @@ def check(path, strict):
 def main():
     args = sys.argv[1:]
     strict = not args
-    paths = args or sorted(glob.glob(os.path.join(ROOT, "profiles", "r04*_bench_*.json")))
+    paths = args or sorted(glob.glob(os.path.join(ROOT, "profiles", "r05*_bench_*.json")))
     bad = []
     for p in paths:
         bad += check(p, strict)

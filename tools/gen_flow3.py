@@ -410,7 +410,7 @@ def emit(spec=0, halfpub=True):
 # Granules (ring edges): 8 B {H-G, (H-G) ^ epoch ^ 0x5BD1E995 ^ (position << 5)} at slot * 8;
 # the position term rejects a slot still holding an earlier round's row (same epoch).
 # ============================================================================================
-RR = 512                 # LDS ring rows per in-workgroup link (sw_flow3.hip F3R_R)
+RR = int(os.environ.get("F3_RR", "512"))   # LDS ring rows per in-workgroup link (sw_flow3.hip F3R_R)
 RING = dict(H="v42", HGO="v43", HB="v44", HGOB="v45", TA="v46", TB="v47", PA="v48", PB="v49", M="v50")
 
 

@@ -37,8 +37,10 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ALGO_BYTES_PER_CELL = 12
-CELLS = {"c2": 65536 * 65536, "c3": 1024 * 8192 * 8192, "c5": (1 << 20) * (1 << 20)}
-WORKLOAD = {"c2": "pair", "c3": "batch", "c5": "slab", "c5p8": "slab_part"}
+CELLS = {"c2": 65536 * 65536, "c3": 1024 * 8192 * 8192, "c5": (1 << 20) * (1 << 20),
+         "c2a": 65536 * 65536, "c5a": (1 << 20) * (1 << 20)}
+# c2a / c5a: the same pairs with the affine constants (2, -3, 5, 2) (bench.py AFFINE_PARAMS)
+WORKLOAD = {"c2": "pair", "c3": "batch", "c5": "slab", "c5p8": "slab_part", "c2a": "pair_affine", "c5a": "slab_affine"}
 
 
 def cells(cfg):
@@ -96,7 +98,8 @@ def valu_mix(kernel):
     s_path = os.path.join(out, base + "-hip-amdgcn-amd-amdhsa-gfx950.s")
     deps = [os.path.join(csrc, f) for f in (base + ".hip", "sw_device.h", "sw_internal.h")]
     if base == "sw_flow3":
-        deps += [os.path.join(csrc, f) for f in ("sw_flow3_loops.inc", "sw_flow3r_loops.inc")]
+        deps += [os.path.join(csrc, f) for f in ("sw_flow3_loops.inc", "sw_flow3r_loops.inc", "sw_flow3a_loops.inc",
+                                                  "sw_flow3ra_loops.inc")]
     if not os.path.exists(s_path) or os.path.getmtime(s_path) < max(os.path.getmtime(d) for d in deps):
         os.makedirs(out, exist_ok=True)
         subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-c",
@@ -127,7 +130,7 @@ def main():
         return mix_only()
     src, rnd = sys.argv[1], sys.argv[2]
     prof = os.path.join(ROOT, "profiles")
-    for cfg in ("c2", "c3", "c5", "c5p8"):
+    for cfg in ("c2", "c3", "c5", "c5p8", "c2a", "c5a"):
         stats = os.path.join(src, "kt_" + cfg, cfg + "_kernel_stats.csv")
         if not os.path.exists(stats):
             print("skip", cfg)

@@ -15,6 +15,8 @@ for w in $which; do
     c3) args="--workload batch --steps 5 --warmup 1"; pargs="--workload batch --steps 3 --warmup 1";;
     c5) args="--workload slab --steps 3 --warmup 1 --cpu-seconds 10"; pargs="--workload slab --steps 2 --warmup 1";;
     c5p8) args="--workload slab --slab-of 8 --steps 3 --warmup 1 --no-cpu-baseline"; pargs="--workload slab --slab-of 8 --steps 2 --warmup 1";;
+    c2a) args="--workload pair --params 2,-3,5,2 --steps 10 --warmup 2 --no-cpu-baseline"; pargs="--workload pair --params 2,-3,5,2 --steps 5 --warmup 1";;
+    c5a) args="--workload slab --params 2,-3,5,2 --steps 3 --warmup 1 --no-cpu-baseline"; pargs="--workload slab --params 2,-3,5,2 --steps 2 --warmup 1";;
   esac
   timeout -k 10 240 python bench.py $args > gpurun_out/prof/bench_$w.json 2> gpurun_out/prof/bench_$w.err
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof/kt_$w -o $w -- python bench.py $pargs --no-cpu-baseline > gpurun_out/prof/kt_$w.log 2>&1
