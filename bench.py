@@ -743,11 +743,16 @@ def main():
                         "score": hs[0], "scores_equal": len(set(hs)) == 1,
                         "entry": "SmithWatermanScoreCUDA (algoGPU.h:9), host buffers: H2D of both sequences, "
                                  "launch, score D2H, synchronous; mean of %d calls" % calls}
-        if rank == 0 and defaults:
-            if workload == "pair" and N == 65536 and "C2" in gold:   # rank 0's pair is the C2 pair
-                parity = "ok" if first == gold["C2"]["score"] else "MISMATCH"
-            elif workload == "slab" and N == 1 << 20 and slab_buf is None and "C5" in gold:
-                parity = "ok" if first == gold["C5"]["score"] else "MISMATCH"
+        # the goldens of the reference's constants (C2, C5) and of AFFINE_PARAMS (C2_affine, C5_affine)
+        gkey = None
+        if rank == 0 and (defaults or params == AFFINE_PARAMS):
+            suffix = "" if defaults else "_affine"
+            if workload == "pair" and N == 65536:   # rank 0's pair is the C2 pair
+                gkey = "C2" + suffix
+            elif workload == "slab" and N == 1 << 20 and slab_buf is None:
+                gkey = "C5" + suffix
+        if gkey is not None and gkey in gold:
+            parity = "ok" if first == gold[gkey]["score"] else "MISMATCH"
         # N=1: the general affine step on the same pair (the automatic plan takes the
         # exact linear-gap step at G_INIT == G_EXT), for reference
         affine = None

@@ -65,7 +65,7 @@ Params g_params;
 std::atomic<long long> g_opt_W{0}, g_opt_C{0}, g_opt_bytes{0}, g_opt_timeout{30}, g_opt_blocks{0}, g_opt_orient{0},
     g_opt_mode{-1}, g_opt_trace{0}, g_opt_duo_f16{1}, g_opt_f2stream{0}, g_opt_ring{-1}, g_opt_ring_rows{4096}, g_opt_f2_wgs{0}, g_opt_f2w{0}, g_opt_f2pwg{-1},
     g_opt_linear{-1}, g_opt_f3{1}, g_opt_slab_plain{0}, g_opt_duo_lds{1}, g_opt_duo_tab{1}, g_opt_duo_roles{1}, g_opt_f3hl{1},
-    g_opt_f3rhl{0}, g_opt_f3a{1}, g_opt_f3slab{1}, g_opt_duo_prio{0};
+    g_opt_f3rhl{0}, g_opt_f3a{1}, g_opt_f3slab{1}, g_opt_duo_prio{0}, g_opt_f3pool{0};
 
 // Longest sequence the engine takes: granule buffers of m rows keep m * 16 in the
 // 32-bit record count of a buffer resource (sw_device.h linear_edge).
@@ -808,6 +808,9 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
     cfg.f3_slab = (use_f3 || use_f3ra) && edge != nullptr;
     if (cfg.f3_slab) cfg.f3_hl = false;   // (the slab roles exist at C = 64, whole-chunk links)
     if (use_f3a) cfg.f3_hl = job.C == 32 && g_opt_f3hl.load() != 0;
+    // the pool loops (no I/O rotation, tools/gen_flow3.py gen_pool) for staged launches with
+    // half-chunk links at C = 32, both steps, when option f3pool = 1 (default 0: measured slower)
+    cfg.f3p = g_opt_f3pool.load() != 0 && cfg.f3_hl && job.C == 32 && !job.ring && (use_f3 || use_f3a);
     cfg.duo_wrap = duo_wrap;
     cfg.duo_tab = duo_tab;
     if (cfg.f2_w2 && job.C == 16 && !use_f3) {
@@ -907,7 +910,7 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
     t_stats.variant = (cfg.duo_f16 ? 1 : 0) | (cfg.f2_stream ? 2 : 0) | (job.ring ? 4 : 0) | (cfg.f2_lin ? 8 : 0) |
                       (cfg.f2_w2 ? 16 : 0) | (cfg.f2_pwg ? 32 : 0) | (cfg.f3 ? 64 : 0) | (cfg.duo_wrap > 0 ? 128 : 0) |
                       (cfg.duo_tab > 0 ? 256 : 0) | (cfg.f3_hl ? 512 : 0) | (cfg.f3a || cfg.f3ra ? 1024 : 0) |
-                      (cfg.f3_slab ? 2048 : 0);
+                      (cfg.f3_slab ? 2048 : 0) | (cfg.f3p ? 4096 : 0);
     t_stats.boundary_bytes = (long long)(job.bnd_granules * sizeof(Granule));
     c->last = s;
     return 0;
@@ -1739,6 +1742,9 @@ int sw_set_option(const char* key, long long v) {
     } else if (k == "f3slab") {   // 1 (default): column slabs on flow3's ring kernel (sw_flow3rs_kernel), 0: flow2
         if (v < 0 || v > 1) return -1;
         g_opt_f3slab = v;
+    } else if (k == "f3pool") {   // 1: flow3 staged C = 32 half-chunk launches on the pool loops (default 0: slower)
+        if (v < 0 || v > 1) return -1;
+        g_opt_f3pool = v;
     } else if (k == "f3a") {   // 1 (default): staged affine-step launches on flow3 (sw_flow3a_kernel), 0: flow2
         if (v < 0 || v > 1) return -1;
         g_opt_f3a = v;
@@ -1792,6 +1798,7 @@ long long sw_get_option(const char* key) {
     if (k == "f3hl") return g_opt_f3hl;
     if (k == "f3rhl") return g_opt_f3rhl;
     if (k == "f3a") return g_opt_f3a;
+    if (k == "f3pool") return g_opt_f3pool;
     if (k == "f3slab") return g_opt_f3slab;
     if (k == "duo_prio") return g_opt_duo_prio;
     return -1;

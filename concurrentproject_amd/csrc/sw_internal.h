@@ -138,6 +138,7 @@ struct LaunchCfg {
     bool f3 = false;        // MODE_FLOW2 staged two-column linear-gap launch on the flow3 kernel (sw_flow3.hip)
     bool f3_hl = false;     // flow3 staged at C = 32: in-workgroup links hand off every half chunk
     bool f3a = false;       // MODE_FLOW2 staged one-column launch with the affine step on flow3 (sw_flow3a_kernel)
+    bool f3p = false;       // flow3 staged on the pool loops (sw_flow3p_kernel: C = 32, f3_hl, no I/O rotation)
     bool f3ra = false;      // MODE_FLOW2 ring-mode two-column launch with the affine step on flow3 (sw_flow3ra_kernel)
     bool f3_slab = false;   // flow3 ring launch of a column slab (sw_flow3rs_kernel / sw_flow3ras_kernel)
     int duo_wrap = 0;       // MODE_DUO at C = 64: > 0 = strip hand-offs in LDS (sw_duo_lds_kernel), this many

@@ -224,3 +224,46 @@ def test_flow3ra_config_c5_affine(engine, golden):
     assert _device_score(engine, a, b) == g["score"]
     st = engine.last_stats()
     assert st["variant"] & 1024 and st["variant"] & 4 and st["boundary_bytes"] < 1 << 30, st
+
+
+# ---- the pool loops (option f3pool = 1, tools/gen_flow3.py gen_pool: no I/O rotation, inflow rows
+# broadcast from LDS into a 32-step register pool, outflow stored by lane 63; off by default:
+# measured slower) -- kept bit-exact on both steps
+
+def test_flow3_pool_option(engine, oracle_mod, golden):
+    rng = np.random.default_rng(57)
+    pairs = _pairs(rng, SHAPES)
+    engine.set_option("orient", 1)
+    engine.set_option("mode", 5)
+    engine.set_option("C", 32)
+    engine.set_option("f3pool", 1)
+    try:
+        for prm in (AFF, (1, -1, 1, 1), (1, -1, 3, 1)):
+            lin = prm[2] == prm[3]
+            engine.set_option("W", 0 if lin else 1)   # linear-gap: flow3's two-column kernel
+            engine.set_option("f2w", 2 if lin else 0)
+            p = engine.Params(*prm)
+            op = oracle_mod.Params(*prm)
+            exp = [oracle_mod.score_linear(a, b, op) for a, b in pairs]
+            got = []
+            for a, b in pairs:
+                got.append(engine.score(a, b, p))
+                st = engine.last_stats()
+                assert st["variant"] & 4096 and st["variant"] & 512 and st["C"] == 32, (prm, st)
+                assert bool(st["variant"] & 64) == lin and bool(st["variant"] & 1024) != lin, (prm, st)
+            assert got == exp, prm
+            for blocks in (1, 3):
+                engine.set_option("blocks", blocks)
+                assert engine.score_batch(pairs, p) == exp, (prm, blocks)
+            engine.set_option("blocks", 0)
+        for k in ("W", "f2w", "C", "orient"):
+            engine.set_option(k, 0)
+        engine.set_option("mode", -1)
+        for key in ("C2", "C2_affine"):
+            g = golden("configs.json")[key]
+            a, b = engine.gen_pair(g["seed"], g["N"])
+            engine.set_params(engine.Params(*g.get("params", (1, -1, 1, 1))))
+            assert _device_score(engine, a, b) == g["score"], key
+            assert engine.last_stats()["variant"] & 4096, key
+    finally:
+        engine.set_option("f3pool", 0)

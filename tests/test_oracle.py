@@ -154,3 +154,17 @@ def test_config_c5_fixture(oracle_mod, golden):
     for eng in ("ref", "wavefront"):
         r = golden("c5_%s.json" % eng)
         assert r["score"] == c["score"] and r["sha256"] == c["sha256"], (eng, r)
+
+
+def test_config_c5_affine_fixture(oracle_mod, golden):
+    """The C5 golden at the affine constants (2, -3, 5, 2): the same pair, scored by the
+    reference's own LazySmith built with those constants (oracle/Makefile refvar, 1 thread,
+    3.5 h) and by the oracle's wavefront restatement; both result files are committed."""
+    c = golden("configs.json")["C5_affine"]
+    a, b = oracle_mod.gen_pair(c["seed"], c["N"])
+    assert _sha(a, b) == c["sha256"] and c["params"] == [2, -3, 5, 2]
+    assert any("reference LazySmith" in s for s in c["pinned_by"]), c["pinned_by"]
+    assert any("swo_wavefront" in s for s in c["pinned_by"]), c["pinned_by"]
+    for eng in ("ref", "wavefront"):
+        r = golden("c5_affine_%s.json" % eng)
+        assert r["score"] == c["score"] and r["sha256"] == c["sha256"] and r["params"] == c["params"], (eng, r)

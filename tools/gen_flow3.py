@@ -87,7 +87,7 @@ OPERAND_CLASS = {
     "m48": "s[0:1]", "lhi": "s[0:1]",
     "G": "s0", "GI": "s0", "GE": "s0", "k80": "s0", "end": "s0", "dlo": "s0", "dhi": "s0", "ek": "s0", "ek2": "s0",
     "m": "s0", "gimask8": "s0", "gomask8": "s0", "gimask16": "s0", "gomask16": "s0", "crv0": "s0", "bpbase": "s0",
-    "fail": "s0", "slow": "s0", "ekp": "s0", "ek2p": "s0",
+    "fail": "s0", "slow": "s0", "ekp": "s0", "ek2p": "s0", "m16": "s[0:1]", "l63": "s[0:1]",
 }
 _SIZE_CACHE = {}
 _PROMOTABLE = ("v_mov_b32", "v_add_u32", "v_sub_u32", "v_subrev_u32", "v_xor_b32", "v_max_i32", "v_max_u32",
@@ -1393,10 +1393,396 @@ def emit_ring_aff():
     return "\n".join(out)
 
 
+# ============================================================================================
+# Pool loops (staged organisation, sw_flow3.hip flow3_staged<..., POOL = true>, the default):
+# the same strips, steps and chunks, WITHOUT the rotating I/O register.  The rotation exists to
+# bring inflow row k to lane 0 at step k and to collect lane 63's outflow: one DPP move per
+# flowing quantity per step (1 of the linear-gap step's 9.5 VALU, 2 of the affine step's
+# 10.75).  Here every step k owns a register P(k) of a 32-step pool:
+#   * inflow: 16-B broadcast LDS reads (one address for the whole wave) put row k into every
+#     lane of P(k) before step k; the step's tied DPP-add (old = P(k)) writes H[l-1] - G into
+#     lanes 1..63 and keeps the inflow in lane 0 -- no move.  No inflow (strip 0): bound_ctrl
+#     zero-fills lane 0's source, so lane 0 gets 0 + (-G), the boundary value;
+#   * diagonal: P(k - 1) is still intact at step k (it was the last step's hgL);
+#   * outflow: after a half chunk lane 63 of P(c) .. P(c + 15) holds rows c - 63 .. c - 48; one
+#     exec-masked (lane 63) run of 16-B LDS writes stores them into the consumer's ring.
+# Per 16 steps this trades 16 (32 affine) DPP moves for 4 (8) reads, 4 (8) writes and 2 SALU.
+# A 16-B group is G rows (4 linear-gap 4-B slots, 2 affine 8-B slots) and 4 aligned pool
+# registers.  Input rows = steps and output rows = steps - 63 cannot both fall on the same
+# 16-row halves of one wave, so wave w of a workgroup runs its halves shifted by SH = w steps
+# (steps [16h + w, 16h + w + 16), pool index (k - w) mod 32): its output halves are then
+# exactly wave w + 1's input halves, and every link's rows [32j + SH_consumer, + 32)
+# ("window" j) occupy the ring slots [(32j + 128) mod R, + 32), contiguous (slot of row r:
+# (r + 128 - SH_consumer) mod R).  The loader writes row r at slot (r + 128) mod R (wave 0
+# runs SH = 0).  Words: prod = rows available (rows < prod are in the
+# ring), cons = rows consumed + R; both move once per half chunk (16 rows), as the half-chunk
+# links did.  The granule role (the group's last strip) writes its halves into its own ring
+# and reads 16 rows back lane-parallel for the 8-B / 16-B granules.
+# ============================================================================================
+POOL_LOW = int(os.environ.get("F3P_LOW", "0"))   # A/B: linear-gap pool at v96..v127, control registers at v48..v63
+POOL_BASE = 128
+POOL_A = int(os.environ.get("F3P_A", "2"))     # steps a half's inflow reads are issued ahead of it
+POOL_WD = int(os.environ.get("F3P_WD", "4"))   # steps the producer-word read runs ahead of the check
+POOL_GS = int(os.environ.get("F3P_GS", "2"))   # steps between a granule read-back and its store
+POOL_PAD = int(os.environ.get("F3P_PAD", "0"))   # A/B probe: 1 s_nop / 2 VALU before the step's DPP-add
+POOL_NOW = int(os.environ.get("F3P_NOW", "0"))   # timing probe only (wrong results): no outflow data writes
+POOL_NOR = int(os.environ.get("F3P_NOR", "0"))   # timing probe only (wrong results): no inflow data reads
+POOL_SCRATCH = int(os.environ.get("F3P_SCRATCH", "1"))   # outflow writes by all lanes, 0..62 into scratch (no exec writes)
+PC = dict(word="v100", caddr="v101", iaddr="v102", oaddr="v104", pval="v105", cval="v107", bp="v108",
+          rbaddr="v109", goff="v110", gmask="v111", rb="v112", rb2="v113", go="v116")
+PC_LOW = dict(word="v48", caddr="v49", iaddr="v50", oaddr="v51", pval="v52", cval="v53", bp="v54",
+              rbaddr="v55", goff="v56", gmask="v57", rb="v58", rb2="v59", go="v60")
+
+
+def _pool_base(aff):
+    return 96 if (POOL_LOW and not aff) else POOL_BASE
+
+
+def _pool_reg(k, PI, aff):
+    idx = (k + PI) % 32
+    return _pool_base(aff) + 2 * idx if aff else _pool_base(aff) + idx
+
+
+def step_pool_lin(a, k, PI, bc):
+    """One step of the two-column linear-gap step on pool register P(k): 8 VALU + the
+    running max (the rotation is gone; sw_flow2.hip step_lin2, main.cpp:54-66)."""
+    P = "v%d" % _pool_reg(k, PI, False)
+    Pp = "v%d" % _pool_reg(k - 1, PI, False)
+    b = k % 4
+    a(f"v_add_u32_sdwa v70, sext(v72), {Pp} dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_{b} src1_sel:DWORD")
+    a(f"v_add_u32_sdwa v71, sext(v73), v66 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_{b} src1_sel:DWORD")
+    if POOL_PAD == 1:
+        a("s_nop 0")
+    elif POOL_PAD == 2:
+        a("v_mov_b32 v119, v119")
+    a(f"v_add_u32_dpp {P}, v68, %[ng] wave_shr:1 row_mask:0xf bank_mask:0xf" + (" bound_ctrl:1" if bc else ""))
+    a(f"v_max3_i32 v66, {P}, v67, v70")
+    a("v_sub_u32_e64 v67, v66, %[G] clamp")
+    a("v_max3_i32 v68, v67, v69, v71")
+    a("v_sub_u32_e64 v69, v68, %[G] clamp")
+    a("v_max3_i32 v74, v74, v70, v71")
+
+
+def step_pool_aff(a, k, PI, bc):
+    """One step of the one-column affine step on pool registers (PH(k), PE(k)): 8 VALU + the
+    running max every other step (step_aff1 without its two rotations)."""
+    r = _pool_reg(k, PI, True)
+    PH, PE = "v%d" % r, "v%d" % (r + 1)
+    PHp = "v%d" % _pool_reg(k - 1, PI, True)
+    t = "v73" if k % 2 == 0 else "v74"
+    z = " bound_ctrl:1" if bc else ""
+    a(f"v_add_u32_sdwa {t}, sext(v75), {PHp} dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_{k % 4} src1_sel:DWORD")
+    a(f"v_add_u32_dpp {PH}, v68, %[ng] wave_shr:1 row_mask:0xf bank_mask:0xf" + z)
+    a(f"v_add_u32_dpp {PE}, v72, %[nge] wave_shr:1 row_mask:0xf bank_mask:0xf" + z)
+    a("v_max3_i32 v70, v71, v69, 0")
+    a(f"v_max_i32 v72, {PE}, {PH}")
+    a(f"v_max3_i32 v68, {t}, v72, v70")
+    a("v_subrev_u32 v71, %[GE], v70")
+    a("v_subrev_u32 v69, %[G], v68")
+    if k % 2:
+        a("v_max3_i32 v76, v76, v73, v74")
+
+
+def resolve_lgkm(items):
+    """items: ("i", text) | ("op", name, text) | ("wait", names).  Each wait becomes the
+    s_waitcnt lgkmcnt(n) that holds until the newest issue of any of `names` (searched back
+    cyclically: the body is a loop) has completed -- LDS ops complete in order."""
+    n = len(items)
+    out = []
+    for i, it in enumerate(items):
+        if it[0] == "i":
+            out.append(it[1])
+        elif it[0] == "op":
+            out.append(it[2])
+        else:
+            cnt = 0
+            for d in range(1, n + 1):
+                j = (i - d) % n
+                if items[j][0] == "op":
+                    if items[j][1] in it[1]:
+                        break
+                    cnt += 1
+            else:
+                raise AssertionError("wait for %s: never issued" % (it[1],))
+            w = "s_waitcnt lgkmcnt(%d)" % min(cnt, 15)
+            if out and out[-1].startswith("s_waitcnt lgkmcnt("):   # merge adjacent waits
+                prev = int(out[-1][len("s_waitcnt lgkmcnt("):-1])
+                out[-1] = "s_waitcnt lgkmcnt(%d)" % min(prev, min(cnt, 15))
+            else:
+                out.append(w)
+    return out
+
+
+def gen_pool(IN, OUT_, SH, aff):
+    """The staged chunk loop of one strip role on the register pool (see above): C = 32-row
+    chunks, a body of two chunks (64 steps), 16-row links.  SH = the wave's index in its
+    workgroup: its halves are the steps [16h + SH, 16h + SH + 16), whose outflow rows are
+    exactly wave SH + 1's halves (rows = steps - 63); pool index of step k = (k - SH) mod 32."""
+    G, SZ = (2, 8) if aff else (4, 4)
+    gsz = 16 if aff else 8                # granule bytes per row
+    PI = -SH
+    PC = PC_LOW if (POOL_LOW and not aff) else globals()["PC"]
+    lds_in, lds_out, gran = IN == "lds", OUT_ == "lds", OUT_ == "gran"
+    A, WD, GS = POOL_A, POOL_WD, POOL_GS
+    ngrp = 16 // G                        # 16-B groups per half
+    ev = {p: [] for p in range(65)}       # items before step p (p = 64: after the last step)
+
+    def base(pos):                        # s40 (k0) at body position pos, relative to the body's first row
+        return 0 if pos < 32 else 32
+
+    def place(e):
+        """body position of an event at step e (relative to its half's body) and the row shift
+        from that body to the one the event runs in"""
+        if e < 0:
+            return e + 64, 64
+        if e > 64:
+            return e - 64, -64
+        return e, 0
+
+    I = lambda t: ("i", t)
+
+    def check(h, c, shift, pos, label):
+        return [("wait", ("w%d" % h,)) if h is not None else I("s_waitcnt lgkmcnt(0)"),
+                I(f"v_readfirstlane_b32 s43, {PC['word']}"),
+                I(f"s_add_u32 s52, s40, {c + 16 + shift - base(pos)}"),
+                I("s_cmp_lt_i32 s43, s52"),
+                I(f"s_cbranch_scc1 L_in{label}_%="),
+                I(f"L_inr{label}_%=:")]
+
+    def reads(h, c, tag):
+        out = []
+        if h % 2 == 0:                    # a new window: ((32 j + 128) mod R) slots
+            out.append(I(f"s_add_u32 s41, s41, {32 * SZ:#x}"))
+            out.append(I(f"s_and_b32 s41, s41, {R * SZ - 1:#x}"))
+            out.append(I(f"v_add_u32 {PC['iaddr']}, s41, %[lin]"))
+        for i in range(ngrp):
+            r = _pool_reg(c + G * i, PI, aff)
+            if POOL_NOR and i > 0:
+                continue
+            out.append(("op", tag, f"ds_read_b128 v[{r}:{r + 3}], {PC['iaddr']} offset:{(h % 2) * 16 * SZ + 16 * i}"))
+        return out
+
+    slow_in = []
+    # ---- consumer: half h covers steps [c, c + 16), c = 16 h + SH
+    if lds_in:
+        for h in range(4):
+            c = 16 * h + SH
+            pw, _ = place(c - A - WD)
+            pc_, sh_c = place(c - A)
+            pd, _ = place(c)
+            ev[pw].append(("op", "w%d" % h, f"ds_read_b32 {PC['word']}, %[pin]"))
+            its = check(h, c, sh_c, pc_, h) + reads(h, c, "d%d" % h)
+            if h % 2 == 1:                # rows < c + 16 consumed: report once per window
+                its.append(I(f"v_add_u32 {PC['cval']}, 32, {PC['cval']}"))
+                its.append(("op", "q%d" % h, f"ds_write_b32 %[qme], {PC['cval']}"))
+            ev[pc_].extend(its)
+            ev[pd].append(("wait", ("d%d" % h,)))
+            slow_in.append(str(h))
+    # ---- producer: half h's outflow (rows c - 63 .. c - 48) once its last step is done
+    if lds_out or gran:
+        for h in range(4):
+            c = 16 * h + SH
+            pe, sh_e = place(c + 16)
+            its = []
+            if h % 2 == 0:
+                if lds_out:               # the window's slots held rows < c - 31 - R
+                    its += [I(f"s_add_u32 s52, s40, {c - 31 + sh_e - base(pe)}"),
+                            I("s_cmp_lt_i32 s44, s52"),
+                            I(f"s_cbranch_scc1 L_bp{h}_%="),
+                            I(f"L_bpr{h}_%=:")]
+                its += [I(f"s_add_u32 s42, s42, {32 * SZ:#x}"),
+                        I(f"s_and_b32 s42, s42, {R * SZ - 1:#x}"),
+                        I(f"v_add_u32 {PC['oaddr']}, s42, %[lout]")]
+                if POOL_SCRATCH:          # lanes 0..62 write into their scratch slots
+                    its.append(I(f"v_cndmask_b32_e64 {PC['oaddr']}, %[lsc], {PC['oaddr']}, %[l63]"))
+                if gran:
+                    its.append(I(f"v_add_u32 {PC['rbaddr']}, s42, %[lrb]"))
+            if not POOL_SCRATCH:
+                its.append(I("s_mov_b64 exec, %[l63]"))
+            for i in range(ngrp):
+                r = _pool_reg(c + G * i, PI, aff)
+                if POOL_NOW and i > 0:
+                    continue
+                its.append(("op", "o%d" % h, f"ds_write_b128 {PC['oaddr']}, v[{r}:{r + 3}] offset:{(h % 2) * 16 * SZ + 16 * i}"))
+            if not POOL_SCRATCH:
+                its.append(I("s_mov_b64 exec, -1"))
+            if lds_out:
+                its.append(I(f"v_add_u32 {PC['pval']}, 16, {PC['pval']}"))
+                its.append(("op", "p%d" % h, f"ds_write_b32 %[pout], {PC['pval']}"))
+            if gran:                      # read the half back lane-parallel (lanes 0..15 = its rows)
+                rb = f"v[{PC['rb'][1:]}:{PC['rb2'][1:]}]" if aff else PC['rb']
+                its.append(("op", "r%d" % h, f"ds_read_b{64 if aff else 32} {rb}, {PC['rbaddr']} offset:{(h % 2) * 16 * SZ}"))
+            ev[pe].extend(its)
+            if gran:
+                ps = min(pe + GS, 64)
+                g = int(PC["go"][1:])
+                st = [("wait", ("r%d" % h,))]
+                if aff:
+                    st += [I(f"v_mov_b32 v{g}, {PC['rb']}"),
+                           I(f"v_xor_b32 v{g + 1}, %[ek], {PC['rb']}"),
+                           I(f"v_mov_b32 v{g + 2}, {PC['rb2']}"),
+                           I(f"v_xor_b32 v{g + 3}, %[ek2], {PC['rb2']}")]
+                else:
+                    st += [I(f"v_xor_b32 {PC['rb2']}, %[ek], {PC['rb']}")]
+                st += [I(f"v_cndmask_b32_e64 {PC['gmask']}, -16, {PC['goff']}, %[m16]"),
+                       I(f"v_add_u32 {PC['goff']}, {16 * gsz:#x}, {PC['goff']}")]
+                if aff:
+                    st.append(I(f"buffer_store_dwordx4 v[{g}:{g + 3}], {PC['gmask']}, %[rsrc], 0 offen sc1"))
+                else:
+                    st.append(I(f"buffer_store_dwordx2 v[{PC['rb'][1:]}:{PC['rb2'][1:]}], {PC['gmask']}, %[rsrc], 0 offen sc1"))
+                ev[ps].extend(st)
+
+    # ---- the body: chunk tops (codes of the next chunk), events, perms, steps
+    body = []
+    for k in range(64):
+        if k == 32:
+            body.append(I("s_add_i32 s40, s40, 32"))
+        if k in (0, 32):
+            body.append(("wait", ("c1",) if k == 0 else ("c0",)))
+            nxt = (84 if not aff else 88) if k == 0 else (76 if not aff else 80)
+            obase = 32 if k == 0 else 64
+            for q in range(2):
+                body.append(("op", "c0" if k == 0 else "c1",
+                             f"ds_read_b128 v[{nxt + 4 * q}:{nxt + 4 * q + 3}], {PC['caddr']} offset:{obase + 16 * q}"))
+        body.extend(ev[k])
+        if k % 4 == 0:
+            cur = (76 if k < 32 else 84) if not aff else (80 if k < 32 else 88)
+            u = (k % 32) // 4
+            if aff:
+                body.append(I(f"v_perm_b32 v75, %[pA], %[k80], v{cur + u}"))
+            else:
+                body.append(I(f"v_perm_b32 v72, %[pA], %[k80], v{cur + u}"))
+                body.append(I(f"v_perm_b32 v73, %[pB], %[k80], v{cur + u}"))
+        lines = []
+        (step_pool_aff if aff else step_pool_lin)(lines.append, k, PI, not lds_in)
+        body.extend(I(t) for t in lines)
+    body.extend(ev[64])
+    body.append(I("s_add_i32 s40, s40, 32"))
+    body.append(I(f"v_add_u32 {PC['caddr']}, 64, {PC['caddr']}"))
+    loop = resolve_lgkm(body)
+
+    L = []
+    a = L.append
+    a("s_nop 4")
+    a("s_waitcnt vmcnt(0) lgkmcnt(0)")
+    if aff:
+        for r in ("v68", "v70", "v72", "v76"):
+            a(f"v_mov_b32 {r}, 0")
+        a("v_mov_b32 v69, %[ng]")
+        a("v_mov_b32 v71, %[nge]")
+        for i in range(32):
+            a(f"v_mov_b32 v{POOL_BASE + 2 * i}, %[ng]")
+            a(f"v_mov_b32 v{POOL_BASE + 2 * i + 1}, %[nge]")
+    else:
+        for r in ("v66", "v67", "v68", "v69", "v74"):
+            a(f"v_mov_b32 {r}, 0")
+        for i in range(32):
+            a(f"v_mov_b32 v{_pool_base(False) + i}, %[ng]")
+    a(f"v_mov_b32 {PC['caddr']}, %[code]")
+    a("s_mov_b32 s40, 0")
+    a(f"s_movk_i32 s41, {96 * SZ:#x}")     # window 0's slots (128) after its first update
+    a(f"s_movk_i32 s42, {32 * SZ:#x}")     # the producer's windows: slots 64 after the first update
+    a("s_mov_b32 s45, 0")
+    a("s_mov_b32 s46, 0")
+    a(f"s_movk_i32 s44, {R}")
+    # (SH > 0: the body's first event writes the last body's half 3, here junk rows < -63)
+    first = SH - 63 - (16 if SH > 0 else 0)
+    if lds_out or gran:   # (the wrapped first write lands in window -3: slots of rows < -63)
+        a(f"v_add_u32 {PC['oaddr']}, s42, %[lout]")
+        if POOL_SCRATCH:
+            a(f"v_cndmask_b32_e64 {PC['oaddr']}, %[lsc], {PC['oaddr']}, %[l63]")
+    if gran:
+        a(f"v_add_u32 {PC['rbaddr']}, s42, %[lrb]")
+    if lds_out:   # rows available after the first publish: first + 16
+        a(f"v_mov_b32 {PC['pval']}, {first & 0xffffffff:#x}")
+    if lds_in:
+        a(f"v_mov_b32 {PC['cval']}, {R + SH}")
+        a(f"v_add_u32 {PC['iaddr']}, s41, %[lin]")   # (the last body's half 3 reads window -1)
+    if gran:
+        a(f"v_mov_b32 {PC['goff']}, %[lrow]")
+    cur0 = 80 if aff else 76
+    for q in range(2):
+        a(f"ds_read_b128 v[{cur0 + 4 * q}:{cur0 + 4 * q + 3}], {PC['caddr']} offset:{16 * q}")
+    if lds_in:   # the halves whose reads the body issues one body early: the last body's half 3, half 0
+        for h in ([-1] if SH > 0 else []) + ([0] if SH - A < 0 else []):
+            c = 16 * h + SH
+            a(f"ds_read_b32 {PC['word']}, %[pin]")
+            for it in check(None, c, 0, 0, "P%d" % (h + 1)) + reads(h % 4, c, "dP"):
+                a(it[1] if it[0] == "i" else it[2])
+            slow_in.append("P%d" % (h + 1))
+    a("s_waitcnt lgkmcnt(0)")
+    a(".p2align 6")
+    a("L_loop_%=:")
+    L.extend(loop)
+    a("s_cmp_lt_i32 s40, %[end]")
+    a("s_cbranch_scc1 L_loop_%=")
+    if lds_out:
+        a(f"v_mov_b32 {PC['pval']}, {BIG:#x}")
+        a(f"ds_write_b32 %[pout], {PC['pval']}")
+    a("s_waitcnt vmcnt(0) lgkmcnt(0)")
+    a("v_mov_b32 %%[M], %s" % ("v76" if aff else "v74"))
+    a("s_mov_b32 %[fail], s45")
+    a("s_mov_b32 %[slow], s46")
+    a("s_branch L_done_%=")
+    for lab in slow_in:
+        slow_wait(a, f"L_in{lab}_%=", f"L_inr{lab}_%=", PC["word"], "%[pin]", "s43", target="s52")
+    if lds_out:
+        for h in (0, 2):
+            slow_wait(a, f"L_bp{h}_%=", f"L_bpr{h}_%=", PC["bp"], "%[qnx]", "s44", target="s52")
+    a("L_done_%=:")
+    return L
+
+
+# the (IN, OUT) roles of each wave of a staged workgroup (shift SH = the wave): wave 0 takes the
+# loader's ring or no inflow, waves 1..3 an LDS ring; waves 0..2 hand on through LDS, wave 3
+# through granules; any wave may hold the pair's last strip (no outflow)
+POOL_ROLES = [(0, "none", "lds"), (0, "none", "none"), (0, "lds", "lds"), (0, "lds", "none"),
+              (1, "lds", "lds"), (1, "lds", "none"), (2, "lds", "lds"), (2, "lds", "none"),
+              (3, "lds", "gran"), (3, "lds", "none")]
+CLOBBERS_POOL = ['"v%d"' % r for r in range(64, 120)] + \
+    ['"s%d"' % r for r in range(40, 53) if r != 47] + ['"scc"', '"vcc"', '"memory"']
+OUT_POOL = os.path.join(ROOT, "concurrentproject_amd", "csrc", "sw_flow3p_loops.inc")
+
+
+def emit_pool():
+    out = ["// GENERATED by tools/gen_flow3.py -- do not edit.  The flow3 pool chunk loops (sw_flow3.hip",
+           "// flow3_staged, POOL): inflow rows broadcast from LDS into a 32-step register pool, outflow by",
+           "// lane 63 under an exec mask, no I/O rotation; C = 32, 16-row links, R = %d ring rows." % R,
+           "// Operands: see F3PLoop in sw_flow3.hip; fixed registers: tools/gen_flow3.py (gen_pool).",
+           "#pragma once", ""]
+    for aff in (False, True):
+        for w, IN, OUT_ in POOL_ROLES:
+            body = align8(gen_pool(IN, OUT_, w, aff))
+            if POOL_LOW and not aff:
+                clob = ['"v%d"' % r for r in range(48, 128)] + CLOBBERS_POOL[56:]
+            else:
+                top = POOL_BASE + (64 if aff else 32)
+                clob = CLOBBERS_POOL + ['"v%d"' % r for r in range(POOL_BASE, top)]
+            out.append("template <> __device__ __forceinline__ F3Res f3p_loop<%d, F3_%s, F3_%s, %d>(const F3PLoop& x) {"
+                       % (int(aff), IN.upper(), OUT_.upper(), w))
+            out.append("    F3Res r;")
+            out.append("    asm volatile(")
+            for line in body:
+                out.append('        "%s\\n\\t"' % line)
+            out.append('        : [M] "=v"(r.M), [fail] "=s"(r.fail), [slow] "=s"(r.slow)')
+            out.append('        : [pA] "v"(x.pA), [pB] "v"(x.pB), [ng] "v"(x.ng), [nge] "v"(x.nge), [G] "s"(x.G),')
+            out.append('          [GE] "s"(x.GE), [k80] "s"(x.k80), [code] "v"(x.code), [lin] "v"(x.lin),')
+            out.append('          [lout] "v"(x.lout), [lrb] "v"(x.lrb), [pin] "v"(x.pin), [pout] "v"(x.pout),')
+            out.append('          [qme] "v"(x.qme), [qnx] "v"(x.qnx), [end] "s"(x.end), [dlo] "s"(x.dlo),')
+            out.append('          [dhi] "s"(x.dhi), [rsrc] "s"(x.rsrc), [ek] "s"(x.ek), [ek2] "s"(x.ek2),')
+            out.append('          [lrow] "v"(x.lrow), [m16] "s"(x.m16), [l63] "s"(x.l63), [lsc] "v"(x.lsc)')
+            out.append("        : " + ", ".join(clob) + ");")
+            out.append("    return r;")
+            out.append("}")
+            out.append("")
+    return "\n".join(out)
+
+
 def main():
     spec = int(os.environ.get("F3_SPEC", "4"))
     halfpub = os.environ.get("F3_HALFPUB", "1") != "0"
     text = emit(spec, halfpub)
+    text_pool = emit_pool()
     text_ring = emit_ring()
     text_aff = emit_aff()
     text_ring_aff = emit_ring_aff()
@@ -1405,7 +1791,11 @@ def main():
         cur_r = open(OUT_RING).read() if os.path.exists(OUT_RING) else ""
         cur_a = open(OUT_AFF).read() if os.path.exists(OUT_AFF) else ""
         cur_ra = open(OUT_RING_AFF).read() if os.path.exists(OUT_RING_AFF) else ""
-        sys.exit(0 if cur == text and cur_r == text_ring and cur_a == text_aff and cur_ra == text_ring_aff else 1)
+        cur_p = open(OUT_POOL).read() if os.path.exists(OUT_POOL) else ""
+        sys.exit(0 if cur == text and cur_r == text_ring and cur_a == text_aff and cur_ra == text_ring_aff and
+                 cur_p == text_pool else 1)
+    with open(OUT_POOL, "w") as f:
+        f.write(text_pool)
     with open(OUT_AFF, "w") as f:
         f.write(text_aff)
     with open(OUT_RING_AFF, "w") as f:

@@ -108,7 +108,7 @@ def main():
     out["slow_chunks_ingroup_mean"] = float(sl[~xg].mean()) if sl.size else None
     out["slow_chunks_crossgroup_mean"] = float(sl[xg].mean()) if xg.any() else None
     print(json.dumps(out))
-    for k in list(range(0, 9)) + list(range(strips - 5, strips)):
+    for k in sorted(set(range(0, min(9, strips))) | set(range(max(0, strips - 5), strips))):
         print(k, int(start[k]), int(first[k]), int(end[k]), int(spins[k]), round(run_ns[k] / steps, 2))
     # pace along the pipeline: ns per step of each strip's run (first inflow -> end)
     ks = list(range(0, strips, max(1, strips // 24)))
