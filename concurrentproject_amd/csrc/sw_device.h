@@ -30,8 +30,8 @@ __device__ __forceinline__ bool spin_expired(int& n, long long t0, long long tic
 }
 
 // Deadline of a spin loop.  The clock (s_memrealtime) is an SMEM round trip far slower than
-// the LDS or L2 poll it guards, so it is read only every 64th poll: read every poll, it set
-// the pace of every late hand-off (r05: a column slab's in-workgroup hops 9.6 us).
+// the LDS or L2 poll it guards, so it is read only every 64th poll (r05; measured neutral on
+// C2, C5 and the column slab).
 struct SpinDeadline {
     long long t0;
     long long ticks;

@@ -202,6 +202,7 @@ struct Job {
     bool f2_stream = false;      // MODE_FLOW2: row codes streamed (rows too long to stage in LDS)
     bool ring = false;           // MODE_FLOW2, one pair: group edges through per-block rings (O(m) state)
     bool f2w2 = false;           // MODE_FLOW2: two columns per lane (strips of 126 new columns, LIN step)
+    bool f2w3 = false;           // ... three (strips of 189; with f2w2: flow3 ring mode only, sw_flow3r3_kernel)
     bool pwg = false;            // MODE_FLOW2 batch: a pair per workgroup (sw_flow2.hip PWG)
 };
 
@@ -367,14 +368,15 @@ bool flow2_w2_wanted(const Job& job, const Params& p) {
 // Re-plan a grouped job for MODE_FLOW2: strips of 64 columns overlapping by one
 // (w2: 128 columns overlapping by two).  pwg: one item per pair, whose workgroup runs all
 // of its strips with LDS hand-offs only (no granule edges).
-void plan_flow2(Job& job, bool w2, bool pwg = false) {
+void plan_flow2(Job& job, bool w2, bool pwg = false, bool w3 = false) {
     job.mode = MODE_FLOW2;
-    job.f2w2 = w2;
+    job.f2w2 = w2 || w3;
+    job.f2w3 = w3;
     job.pwg = pwg;
     uint64_t g = 0;
     for (size_t k = 0; k < job.pairs.size(); ++k) {
         PairDesc& d = job.pairs[k];
-        d.strips = w2 ? flow2_strips_w2(d.n) : flow2_strips(d.n);
+        d.strips = w3 ? flow2_strips_w3(d.n) : w2 ? flow2_strips_w2(d.n) : flow2_strips(d.n);
         d.bnd_off = g;
         if (!pwg) g += (uint64_t)((d.strips + 3) / 4 - 1) * (uint64_t)d.m;
         job.item_base[k + 1] = job.item_base[k] + (pwg ? 1 : (d.strips + 3) / 4);
@@ -465,6 +467,15 @@ int finalize_mode(Job& job, const Params& prm, int cus) {
             if (job.slab && g_opt_f3slab.load() != 0 && (lin ? g_opt_f3.load() != 0 : g_opt_f3a.load() != 0) &&
                 g_opt_f2w.load() != 1 && g_opt_ring.load() != 0 && (g_opt_C.load() == 0 || g_opt_C.load() == 64)) {
                 if (!job.f2w2) plan_flow2(job, true);
+                job.ring = true;
+            }
+            // three columns per lane (flow3 ring mode, linear-gap step, C = 64; option f2w = 0 or 3): a
+            // third fewer strips at 12.5 VALU per 192 cells instead of 9 per 128. C5 165.0 -> 159.5 ms;
+            // slab 0 of 8 38.6 -> 33.1 ms (its 1041 two-column strips need 261 groups for 256 CUs, and
+            // the 5 CUs running two pace the chain; 694 three-column strips fit 174 groups)
+            if (job.ring && job.f2w2 && lin && (g_opt_f2w.load() == 3 || g_opt_f2w.load() == 0) && g_opt_f3.load() != 0 &&
+                g_opt_f3rhl.load() == 0 && (g_opt_C.load() == 0 || g_opt_C.load() == 64)) {
+                plan_flow2(job, true, false, true);
                 job.ring = true;
             }
             job.f2_stream = job.ring || !flow2_staged(job, max_m);   // ring mode runs with streamed codes
@@ -569,7 +580,7 @@ int plan_slab(Job& job, int n, int m, bool dna, const Params& prm) {
         set_err("a column slab needs a grouped kernel (chain, flow or flow2), not mode %d", job.mode);
         return -1;
     }
-    return job.mode == MODE_FLOW2 ? (job.f2w2 ? 126 : 63) : 64 * job.W;
+    return job.mode == MODE_FLOW2 ? (job.f2w3 ? 189 : job.f2w2 ? 126 : 63) : 64 * job.W;
 }
 
 // Alphabet of a slab call: stated by the caller, never scanned, because every
@@ -729,6 +740,7 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
         probe.f2_w2 = job.f2w2;
         probe.f3_hl = use_f3 && job.C == 64 && g_opt_f3rhl.load() != 0;
         probe.f3ra = use_f3ra;
+        probe.f3_w3 = use_f3 && job.f2w3;
         probe.f3_slab = (use_f3 || use_f3ra) && edge != nullptr;
         if (probe.f3_slab) probe.f3_hl = false;
         int fit = 0;
@@ -811,6 +823,11 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
     // the pool loops (no I/O rotation, tools/gen_flow3.py gen_pool) for staged launches with
     // half-chunk links at C = 32, both steps, when option f3pool = 1 (default 0: measured slower)
     cfg.f3p = g_opt_f3pool.load() != 0 && cfg.f3_hl && job.C == 32 && !job.ring && (use_f3 || use_f3a);
+    cfg.f3_w3 = job.f2w3;
+    if (job.f2w3 && !(use_f3 && job.ring && job.C == 64 && !cfg.f3_hl)) {
+        set_err("three columns per lane run on flow3's ring kernel only (linear-gap step, C = 64, whole-chunk links)");
+        return -1;
+    }
     cfg.duo_wrap = duo_wrap;
     cfg.duo_tab = duo_tab;
     if (cfg.f2_w2 && job.C == 16 && !use_f3) {
@@ -910,7 +927,7 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
     t_stats.variant = (cfg.duo_f16 ? 1 : 0) | (cfg.f2_stream ? 2 : 0) | (job.ring ? 4 : 0) | (cfg.f2_lin ? 8 : 0) |
                       (cfg.f2_w2 ? 16 : 0) | (cfg.f2_pwg ? 32 : 0) | (cfg.f3 ? 64 : 0) | (cfg.duo_wrap > 0 ? 128 : 0) |
                       (cfg.duo_tab > 0 ? 256 : 0) | (cfg.f3_hl ? 512 : 0) | (cfg.f3a || cfg.f3ra ? 1024 : 0) |
-                      (cfg.f3_slab ? 2048 : 0) | (cfg.f3p ? 4096 : 0);
+                      (cfg.f3_slab ? 2048 : 0) | (cfg.f3p ? 4096 : 0) | (cfg.f3_w3 ? 8192 : 0);
     t_stats.boundary_bytes = (long long)(job.bnd_granules * sizeof(Granule));
     c->last = s;
     return 0;
@@ -1715,8 +1732,9 @@ int sw_set_option(const char* key, long long v) {
     } else if (k == "f2_wgs") {   // flow2 streamed kernel: workgroups per CU, 0 = auto, 1..F2_WGS_MAX
         if (v < 0 || v > F2_WGS_MAX) return -1;
         g_opt_f2_wgs = v;
-    } else if (k == "f2w") {   // flow2 columns per lane: 0 auto, 1, 2 (2: the linear-gap step only)
-        if (v < 0 || v > 2) return -1;
+    } else if (k == "f2w") {   // flow2 columns per lane: 0 auto, 1, 2 (2: the linear-gap step only),
+        // 3 (flow3 ring mode with the linear-gap step: single long pairs and column slabs; auto there)
+        if (v < 0 || v > 3) return -1;
         g_opt_f2w = v;
     } else if (k == "f2pwg") {   // int32 DNA batches on flow2, a pair per workgroup: -1 auto, 0 off, 1 forced
         if (v < -1 || v > 1) return -1;

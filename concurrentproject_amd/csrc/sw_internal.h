@@ -139,6 +139,7 @@ struct LaunchCfg {
     bool f3_hl = false;     // flow3 staged at C = 32: in-workgroup links hand off every half chunk
     bool f3a = false;       // MODE_FLOW2 staged one-column launch with the affine step on flow3 (sw_flow3a_kernel)
     bool f3p = false;       // flow3 staged on the pool loops (sw_flow3p_kernel: C = 32, f3_hl, no I/O rotation)
+    bool f3_w3 = false;     // flow3 ring mode at three columns per lane (sw_flow3r3_kernel / sw_flow3r3s_kernel)
     bool f3ra = false;      // MODE_FLOW2 ring-mode two-column launch with the affine step on flow3 (sw_flow3ra_kernel)
     bool f3_slab = false;   // flow3 ring launch of a column slab (sw_flow3rs_kernel / sw_flow3ras_kernel)
     int duo_wrap = 0;       // MODE_DUO at C = 64: > 0 = strip hand-offs in LDS (sw_duo_lds_kernel), this many
@@ -184,6 +185,8 @@ __host__ __device__ constexpr int flow_stage_max(int W, int C) { return LDS_PER_
 __host__ __device__ constexpr int flow2_strips(int n) { return n <= 64 ? 1 : (n - 1 + 62) / 63; }
 // two columns per lane (LaunchCfg::f2_w2): strip s covers columns [126s, 126s + 128)
 __host__ __device__ constexpr int flow2_strips_w2(int n) { return n <= 128 ? 1 : (n - 2 + 125) / 126; }
+// three columns per lane (flow3 ring mode): strips of 189 new columns overlapping by three
+__host__ __device__ constexpr int flow2_strips_w3(int n) { return n <= 192 ? 1 : (n - 3 + 188) / 189; }
 __host__ __device__ constexpr int flow2_stage_bytes(int m, int C) {
     return (64 + ((m + 64 + C - 1) / C + 1) * C + 8 + 15) & ~15;
 }

@@ -162,10 +162,13 @@ def test_flow3_ring_parity(engine, oracle_mod, _ring_reset):
     for prm in (engine.Params(), engine.Params(2, -3, 4, 4), engine.Params(1, 0, 0, 0)):
         op = oracle_mod.Params(prm.match, prm.mismatch, prm.gap_init, prm.gap_ext)
         exp = [oracle_mod.score_linear(a, b, op) for a, b in pairs]
-        # 64-row chunks (automatic in ring mode), 32 (option C), 64 with half-chunk LDS links
-        for C, hl in ((64, 0), (32, 0), (64, 1)):
+        # 64-row chunks (automatic in ring mode) at two columns per lane (option f2w = 2) and at
+        # three (automatic, tests/test_ring_w3.py), 32 (option C), 64 with half-chunk LDS links
+        for C, hl, f2w in ((64, 0, 2), (64, 0, 0), (32, 0, 0), (64, 1, 0)):
             engine.set_option("C", 0 if C == 64 else C)
             engine.set_option("f3rhl", hl)
+            engine.set_option("f2w", f2w)
+            w3 = C == 64 and not hl and f2w == 0
             for blocks, rows in ((0, 4096), (1, 512), (2, 512), (3, 1024), (7, 512)):
                 _ring_opts(engine, blocks, rows)
                 got = []
@@ -176,8 +179,10 @@ def test_flow3_ring_parity(engine, oracle_mod, _ring_reset):
                     if groups > 1:
                         assert st["variant"] & 64 and st["variant"] & 4 and st["C"] == C, st
                         assert bool(st["variant"] & 512) == bool(hl), st
-                assert got == exp, (prm, C, blocks, rows)
+                        assert bool(st["variant"] & 8192) == w3, st
+                assert got == exp, (prm, C, f2w, blocks, rows)
         engine.set_option("C", 0)
+        engine.set_option("f2w", 0)
 
 
 def test_flow3_ring_matches_flow2(engine, _ring_reset):

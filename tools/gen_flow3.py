@@ -45,7 +45,7 @@ ROLES_IN = ("none", "lds")
 MID_AHEAD = int(os.environ.get("F3_MIDAHEAD", "1"))
 LOOP_PAD = int(os.environ.get("F3_LOOP_PAD", "0"))
 RING_ALIGN = int(os.environ.get("F3_RING_ALIGN", "0"))   # A/B: align the ring loops too
-RING_NOPS = int(os.environ.get("F3_RING_NOPS", "0"))   # 4-B s_nop 0 between the 64-B boundary and the loop (A/B)   # 4-step groups the mid-chunk inflow read runs ahead
+RING_NOPS = int(os.environ.get("F3_RING_NOPS", "0"))   # A/B: alignment nops in the ring loops (0: re-encodings only)
 ROLES_OUT = ("none", "lds", "gran")
 
 
@@ -412,6 +412,34 @@ def emit(spec=0, halfpub=True):
 # ============================================================================================
 RR = int(os.environ.get("F3_RR", "512"))   # LDS ring rows per in-workgroup link (sw_flow3.hip F3R_R)
 RING = dict(H="v42", HGO="v43", HB="v44", HGOB="v45", TA="v46", TB="v47", PA="v48", PB="v49", M="v50")
+# three columns per lane (ring mode, sw_flow3.hip flow3_ring<..., W3>): column C's H, max(H_C - G, 0),
+# its t of even / odd steps and score bytes
+RING3 = dict(RING, HC="v108", HGOC="v109", TC0="v110", TC1="v111", PC="v112")
+
+
+def step3(a, io, l0, b, r):
+    """One anti-diagonal step of the three-column linear-gap step (12.5 VALU, 192 cells): columns
+    A, B, C = 3 lane, + 1, + 2; the left input of A is lane l-1's column C (the DPP-add), of B and
+    C the clamped H - G of A and B in the same lane; the running max takes column C's t of two
+    steps in one max3 (odd steps)."""
+    tc = r["TC1"] if b % 2 else r["TC0"]
+    a(f"v_add_u32_sdwa {r['TA']}, sext({r['PA']}), {l0} dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_{b} "
+      "src1_sel:DWORD")
+    a(f"v_add_u32_sdwa {r['TB']}, sext({r['PB']}), {r['H']} dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_{b} "
+      "src1_sel:DWORD")
+    a(f"v_add_u32_sdwa {tc}, sext({r['PC']}), {r['HB']} dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_{b} "
+      "src1_sel:DWORD")
+    a(f"v_mov_b32_dpp {l0}, {io} wave_shl:1 row_mask:0xf bank_mask:0xf")
+    a(f"v_add_u32_dpp {io}, {r['HC']}, %[ng] wave_shr:1 row_mask:0xf bank_mask:0xf")
+    a(f"v_max3_i32 {r['H']}, {io}, {r['HGO']}, {r['TA']}")
+    a(f"v_sub_u32_e64 {r['HGO']}, {r['H']}, %[G] clamp")
+    a(f"v_max3_i32 {r['HB']}, {r['HGO']}, {r['HGOB']}, {r['TB']}")
+    a(f"v_sub_u32_e64 {r['HGOB']}, {r['HB']}, %[G] clamp")
+    a(f"v_max3_i32 {r['HC']}, {r['HGOB']}, {r['HGOC']}, {tc}")
+    a(f"v_sub_u32_e64 {r['HGOC']}, {r['HC']}, %[G] clamp")
+    a(f"v_max3_i32 {r['M']}, {r['M']}, {r['TA']}, {r['TB']}")
+    if b % 2:
+        a(f"v_max3_i32 {r['M']}, {r['M']}, {r['TC0']}, {r['TC1']}")
 
 
 def ring_granule(a, key="%[ek]", cp="sc1"):
@@ -444,7 +472,7 @@ def ring_gin_check(a, C=64, key="%[ek]"):
     a("s_cmp_lg_u64 s[50:51], 0")
 
 
-def gen_role_ring(IN, OUT_, C=64, hl=False):
+def gen_role_ring(IN, OUT_, C=64, hl=False, W=2):
     """The ring-mode loop of one strip role at C-row chunks (64, or 32: half the hand-off
     lag).  The loop body is two chunks; the code ring is refilled 64 rows per body.
     hl (C = 64): half-chunk LDS links as in gen_role: the producer also publishes its newest
@@ -467,7 +495,8 @@ def gen_role_ring(IN, OUT_, C=64, hl=False):
     # ---- entry (s_nop 4: descriptor operands may be fresh from v_readfirstlane)
     a("s_nop 4")
     a("s_waitcnt vmcnt(0) lgkmcnt(0)")
-    for r in ("v42", "v43", "v44", "v45", "v50"):
+    assert W in (2, 3) and (W == 2 or (C == 64 and not hl))
+    for r in ("v42", "v43", "v44", "v45", "v50") + (("v108", "v109") if W == 3 else ()):
         a(f"v_mov_b32 {r}, 0")
     a("v_mov_b32 v40, %[ng]")
     a("v_mov_b32 v41, %[ng]")
@@ -629,9 +658,14 @@ def gen_role_ring(IN, OUT_, C=64, hl=False):
                     a("v_cndmask_b32_e64 v40, v102, v40, %[lhi]")
             a(f"v_perm_b32 v48, %[pA], %[k80], v{cur + u}")
             a(f"v_perm_b32 v49, %[pB], %[k80], v{cur + u}")
+            if W == 3:
+                a(f"v_perm_b32 v112, %[pC], %[k80], v{cur + u}")
             for b in range(4):
                 io, l0 = ("v40", "v41") if b % 2 == 0 else ("v41", "v40")
-                step(a, io, l0, b, RING)
+                if W == 3:
+                    step3(a, io, l0, b, RING3)
+                else:
+                    step(a, io, l0, b, RING)
             if gout and C == 64 and u == 7:
                 ring_granule(a, kout, cout)
         # 9. on to the next chunk
@@ -694,9 +728,9 @@ def gen_role_ring(IN, OUT_, C=64, hl=False):
 
 def slow_timeout(a, label):
     """The end of a slow-path poll: sleep and poll again ({label}_w); every 64th poll also reads
-    the clock and gives up past the deadline ({label}_x).  s_memrealtime is an SMEM round trip
-    much slower than an LDS poll: read every poll, it set the pace of every late hand-off (a
-    column slab's in-workgroup hops took 9.6 us, r05)."""
+    the clock and gives up past the deadline ({label}_x).  s_memrealtime is an SMEM round trip,
+    much slower than an LDS poll, so a late hand-off no longer pays one per poll (measured neutral
+    on C2, C5 and the column slab, r05)."""
     a("s_add_u32 s46, s46, 1")
     a("s_and_b32 s48, s46, 63")
     a("s_cmp_lg_u32 s48, 0")
@@ -795,6 +829,42 @@ def emit_ring():
 
 
 OUT_RING = os.path.join(ROOT, "concurrentproject_amd", "csrc", "sw_flow3r_loops.inc")
+OUT_RING3 = os.path.join(ROOT, "concurrentproject_amd", "csrc", "sw_flow3r3_loops.inc")
+CLOBBERS_RING3 = CLOBBERS_RING + ['"v%d"' % r for r in range(108, 113)]
+
+
+def emit_ring3():
+    """Three columns per lane in ring mode (sw_flow3.hip flow3_ring<64, 0, false, SLAB, true>):
+    C = 64, whole-chunk links, every ring role and the column-slab roles."""
+    out = ["// GENERATED by tools/gen_flow3.py -- do not edit.  The flow3 ring-mode chunk loops at three",
+           "// columns per lane (sw_flow3.hip sw_flow3r3_kernel): one inline-asm block per strip role, C = 64, R = %d." % RR,
+           "// Operands: see F3RLoop in sw_flow3.hip; fixed registers: tools/gen_flow3.py (RING3).",
+           "#pragma once", ""]
+    for IN, OUT_ in [(i, o) for i in ROLES_IN_RING for o in ROLES_OUT] + list(ROLES_SLAB):
+        body = gen_role_ring(IN, OUT_, 64, False, 3)
+        out.append("template <> __device__ __forceinline__ F3Res f3r3_loop<F3_%s, F3_%s>(const F3RLoop& x) {"
+                   % (IN.upper(), OUT_.upper()))
+        out.append("    F3Res r;")
+        out.append("    asm volatile(")
+        for line in body:
+            out.append('        "%s\\n\\t"' % line)
+        out.append('        : [M] "=v"(r.M), [fail] "=s"(r.fail), [slow] "=s"(r.slow)')
+        out.append('        : [pA] "v"(x.pA), [pB] "v"(x.pB), [pC] "v"(x.pC), [ng] "v"(x.ng), [G] "s"(x.G), [k80] "s"(x.k80),')
+        out.append('          [m] "s"(x.m), [end] "s"(x.end), [dlo] "s"(x.dlo), [dhi] "s"(x.dhi), [lane] "v"(x.lane),')
+        out.append('          [raw2] "v"(x.raw2), [cro] "v"(x.cro), [c0] "v"(x.c0), [cbase] "v"(x.cbase),')
+        out.append('          [cwr] "v"(x.cwr), [cwm] "v"(x.cwm), [rrs] "s"(x.rrs), [rrow] "v"(x.rrow),')
+        out.append('          [lin] "v"(x.lin), [lout] "v"(x.lout), [pin] "v"(x.pin), [pout] "v"(x.pout),')
+        out.append('          [qme] "v"(x.qme), [qnx] "v"(x.qnx),')
+        out.append('          [girs] "s"(x.girs), [gioff] "v"(x.gioff), [gipos] "v"(x.gipos), [gimask8] "s"(x.gimask8),')
+        out.append('          [ek] "s"(x.ek), [cross] "s"(x.cross), [crv0] "s"(x.crv0), [croff] "v"(x.croff),')
+        out.append('          [gors] "s"(x.gors), [gooff] "v"(x.gooff), [gopos] "v"(x.gopos), [gomask8] "s"(x.gomask8),')
+        out.append('          [gorow] "v"(x.gorow), [lhi] "s"(x.lhi), [bpr] "s"(x.bpr), [bpbase] "s"(x.bpbase),')
+        out.append('          [lmid] "v"(x.lmid), [ekp] "s"(x.ekp)')
+        out.append("        : " + ", ".join(CLOBBERS_RING3) + ");")
+        out.append("    return r;")
+        out.append("}")
+        out.append("")
+    return "\n".join(out)
 
 # ============================================================================================
 # The general affine (Gotoh) step, staged organisation (C2 with G_INIT != G_EXT):
@@ -1783,6 +1853,7 @@ def main():
     halfpub = os.environ.get("F3_HALFPUB", "1") != "0"
     text = emit(spec, halfpub)
     text_pool = emit_pool()
+    text_ring3 = emit_ring3()
     text_ring = emit_ring()
     text_aff = emit_aff()
     text_ring_aff = emit_ring_aff()
@@ -1792,10 +1863,13 @@ def main():
         cur_a = open(OUT_AFF).read() if os.path.exists(OUT_AFF) else ""
         cur_ra = open(OUT_RING_AFF).read() if os.path.exists(OUT_RING_AFF) else ""
         cur_p = open(OUT_POOL).read() if os.path.exists(OUT_POOL) else ""
+        cur_r3 = open(OUT_RING3).read() if os.path.exists(OUT_RING3) else ""
         sys.exit(0 if cur == text and cur_r == text_ring and cur_a == text_aff and cur_ra == text_ring_aff and
-                 cur_p == text_pool else 1)
+                 cur_p == text_pool and cur_r3 == text_ring3 else 1)
     with open(OUT_POOL, "w") as f:
         f.write(text_pool)
+    with open(OUT_RING3, "w") as f:
+        f.write(text_ring3)
     with open(OUT_AFF, "w") as f:
         f.write(text_aff)
     with open(OUT_RING_AFF, "w") as f:
