@@ -189,7 +189,10 @@ void sw_db_close(sw_db* db);
  *   "linear"   -1 = (default) the exact linear-gap step when G_INIT == G_EXT
  *              (flow2 C = 32 or 64, f16 duos), 0 = always the affine step
  *   "f2w"      flow2 columns per lane: 0 = (default) two whenever the linear-gap
- *              step runs, one otherwise; 1 = always one; 2 = two (linear-gap step only)
+ *              step runs (three in flow3 ring mode: C5, column slabs), one otherwise;
+ *              1 = always one; 2 = two (linear-gap step only); 3 = three where ring mode runs
+ *   "f3pool"   1 = flow3 staged launches on the loops without the I/O rotation (measured
+ *              slower; default 0)
  *   "ring"     -1 = (default) ring edges for a single flow2 pair whose linear edges
  *              would exceed 1 GB, 0 = never, 1 = always (one pair per launch)
  *   "ring_rows" rows per within-round ring, a power of two in [512, 2^20] (4096)

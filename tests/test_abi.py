@@ -67,15 +67,22 @@ def test_options_host_side():
 
 
 def test_slab_bounds_host_side():
-    """Column-slab planning (host only): flow2 slabs are multiples of its 63-column
-    stride, the chain / flow kernels' of 64*W; the alphabet must be stated."""
+    """Column-slab planning (host only): flow2 / flow3 slabs are multiples of their strip
+    stride (63 columns per lane-column; 189 at three columns per lane, the automatic
+    slab kernel), the chain / flow kernels' of 64*W; the alphabet must be stated."""
     import concurrentproject_amd as sw
     sw.set_params(sw.Params())
     b = sw.slab_bounds(65536, 65536, 4, sw.SW_FLAG_DNA)          # rows fit in LDS: flow2
     assert b[0] == 0 and b[-1] == 65536 and all(x % 63 == 0 for x in b[1:-1]) and b == sorted(b)
-    b = sw.slab_bounds(1 << 20, 1 << 20, 8, sw.SW_FLAG_DNA)      # C5: flow2 streaming its row codes
-    assert b[-1] == 1 << 20 and all(x % 63 == 0 for x in b[1:-1]) and len(set(b)) == 9
-    assert max(y - x for x, y in zip(b, b[1:])) - min(y - x for x, y in zip(b, b[1:])) < 8 * 63
+    b = sw.slab_bounds(1 << 20, 1 << 20, 8, sw.SW_FLAG_DNA)      # C5: flow3 ring slabs, three columns per lane
+    assert b[-1] == 1 << 20 and all(x % 189 == 0 for x in b[1:-1]) and len(set(b)) == 9
+    assert max(y - x for x, y in zip(b, b[1:])) - min(y - x for x, y in zip(b, b[1:])) < 8 * 189
+    sw.set_option("f2w", 2)                                      # two columns per lane: 126-column multiples
+    try:
+        b = sw.slab_bounds(1 << 20, 1 << 20, 8, sw.SW_FLAG_DNA)
+        assert all(x % 126 == 0 for x in b[1:-1]) and b[-1] == 1 << 20
+    finally:
+        sw.set_option("f2w", 0)
     sw.set_option("mode", 2)                                     # forced chain: 64*W columns
     try:
         b = sw.slab_bounds(1 << 20, 1 << 20, 8, sw.SW_FLAG_DNA)
