@@ -665,7 +665,8 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
     //   N = 2^19 (2080)         116 83.9 80.1 78.9  | 117 83.2 88.5 96.2
     //   N = 2^20 (4162, C5)     437 312 287 283     | 454 307 299 -
     // ring: one per 2 CUs' worth of groups, up to 4, or one round of all groups when they fit
-    // (below); linear edges: 2 from 4 groups per CU
+    // (below); three columns per lane: 4 (C5's 1388 groups: 2 / 3 / 4 per CU 159.5 / 156.6 /
+    // 155.6 ms; 694 or 925 blocks 166.4 / 159.3); linear edges: 2 from 4 groups per CU
     int f2_wgs = 1;
     if (f2s) {
         const long long o = g_opt_f2_wgs.load();
@@ -674,7 +675,7 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
         // (ceil: cus < P < 2 cus needs 2 per CU, not a second pass of P - cus pairs)
         const int per_cu_ceil = (job.item_base[np] + c->cus - 1) / c->cus;
         f2_wgs = o > 0           ? (int)o
-                 : job.ring      ? (job.item_base[np] <= c->cus * F2_WGS_MAX ? F2_WGS_MAX
+                 : job.ring      ? (job.item_base[np] <= c->cus * F2_WGS_MAX || job.f2w3 ? F2_WGS_MAX
                                                                              : std::min(F2_WGS_MAX, std::max(1, per_cu / 2)))
                  : job.pwg       ? std::min({F2_WGS_MAX, std::max(1, per_cu_ceil),
                                              flow2_pwg_wgs(max_m_all, job.C, job.f2w2)})

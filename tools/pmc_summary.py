@@ -99,7 +99,7 @@ def valu_mix(kernel):
     deps = [os.path.join(csrc, f) for f in (base + ".hip", "sw_device.h", "sw_internal.h")]
     if base == "sw_flow3":
         deps += [os.path.join(csrc, f) for f in ("sw_flow3_loops.inc", "sw_flow3r_loops.inc", "sw_flow3a_loops.inc",
-                                                  "sw_flow3ra_loops.inc")]
+                                                  "sw_flow3ra_loops.inc", "sw_flow3p_loops.inc", "sw_flow3r3_loops.inc")]
     if not os.path.exists(s_path) or os.path.getmtime(s_path) < max(os.path.getmtime(d) for d in deps):
         os.makedirs(out, exist_ok=True)
         subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-c",
