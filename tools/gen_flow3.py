@@ -45,6 +45,7 @@ ROLES_IN = ("none", "lds")
 MID_AHEAD = int(os.environ.get("F3_MIDAHEAD", "1"))
 LOOP_PAD = int(os.environ.get("F3_LOOP_PAD", "0"))
 RING_ALIGN = int(os.environ.get("F3_RING_ALIGN", "0"))   # A/B: align the ring loops too
+STAGED_PROMOTE = int(os.environ.get("F3_PROMOTE", "1"))   # A/B: staged alignment by VOP3 re-encoding (1) or s_nop only (0)
 RING_NOPS = int(os.environ.get("F3_RING_NOPS", "0"))   # A/B: alignment nops in the ring loops (0: re-encodings only)
 ROLES_OUT = ("none", "lds", "gran")
 
@@ -120,10 +121,11 @@ def _sizes(lines):
             for l in lines]
 
 
-def align8(lines, nops=True):
+def align8(lines, nops=True, promote=True):
     """The loop of an asm block (from its 64-B aligned L_loop label to the loop's back branch)
     with every 8-B instruction on an 8-B boundary (see above); nops = False: re-encodings only
-    (an 8-B instruction after a run without a promotable one stays where it is)."""
+    (an 8-B instruction after a run without a promotable one stays where it is); promote =
+    False: s_nop padding only."""
     try:
         i0 = lines.index("L_loop_%=:")
         i1 = lines.index("s_cbranch_scc1 L_loop_%=")
@@ -134,7 +136,7 @@ def align8(lines, nops=True):
     out, off, cand = [], 0, None        # cand: index in out of the last promotable 4-B VALU since an 8-B one
     for l, n in zip(body, sz):
         if n == 8 and off % 8 == 4:
-            if cand is not None:
+            if cand is not None and promote:
                 op, rest = out[cand].split(" ", 1)
                 out[cand] = op + "_e64 " + rest
                 off += 4
@@ -373,7 +375,7 @@ def emit(spec=0, halfpub=True):
     for C, hl in ((32, 0), (16, 0), (32, 1)):
         for IN in ROLES_IN:
             for OUT_ in ROLES_OUT:
-                body = align8(gen_role(IN, OUT_, spec, halfpub, C, bool(hl)))
+                body = align8(gen_role(IN, OUT_, spec, halfpub, C, bool(hl)), promote=STAGED_PROMOTE)
                 out.append("template <> __device__ __forceinline__ F3Res f3_loop<%d, %d, F3_%s, F3_%s>(const F3Loop& x) {"
                            % (C, hl, IN.upper(), OUT_.upper()))
                 out.append("    F3Res r;")
@@ -840,10 +842,17 @@ def emit_ring3():
            "// columns per lane (sw_flow3.hip sw_flow3r3_kernel): one inline-asm block per strip role, C = 64, R = %d." % RR,
            "// Operands: see F3RLoop in sw_flow3.hip; fixed registers: tools/gen_flow3.py (RING3).",
            "#pragma once", ""]
-    for IN, OUT_ in [(i, o) for i in ROLES_IN_RING for o in ROLES_OUT] + list(ROLES_SLAB):
+    # ALN = 1 (the column-slab kernel, one wave per SIMD): every 8-B instruction on an 8-B boundary,
+    # padding with s_nop (slab 0 of 8: 32.5 -> 29.5 ms); ALN = 0 (C5, 4 waves per SIMD): as generated
+    # (aligned there: 154.3 -> 161.1 ms with nops, 163.0 with VOP3 re-encodings)
+    combos = [(i, o, 0) for i in ROLES_IN_RING for o in ROLES_OUT] + \
+        [(i, o, 1) for i in ROLES_IN_RING for o in ROLES_OUT] + [(i, o, 1) for i, o in ROLES_SLAB]
+    for IN, OUT_, aln in combos:
         body = gen_role_ring(IN, OUT_, 64, False, 3)
-        out.append("template <> __device__ __forceinline__ F3Res f3r3_loop<F3_%s, F3_%s>(const F3RLoop& x) {"
-                   % (IN.upper(), OUT_.upper()))
+        if aln:
+            body = align8(body, nops=True, promote=False)
+        out.append("template <> __device__ __forceinline__ F3Res f3r3_loop<F3_%s, F3_%s, %d>(const F3RLoop& x) {"
+                   % (IN.upper(), OUT_.upper(), aln))
         out.append("    F3Res r;")
         out.append("    asm volatile(")
         for line in body:
@@ -1093,7 +1102,7 @@ def emit_aff():
     for C, hl in ((32, 1), (32, 0), (16, 0)):
         for IN in ROLES_IN:
             for OUT_ in ROLES_OUT:
-                body = align8(gen_role_aff(IN, OUT_, C, bool(hl)))
+                body = align8(gen_role_aff(IN, OUT_, C, bool(hl)), promote=STAGED_PROMOTE)
                 out.append("template <> __device__ __forceinline__ F3Res f3a_loop<%d, %d, F3_%s, F3_%s>(const F3ALoop& x) {"
                            % (C, hl, IN.upper(), OUT_.upper()))
                 out.append("    F3Res r;")
