@@ -473,8 +473,8 @@ int finalize_mode(Job& job, const Params& prm, int cus) {
             // third fewer strips at 12.5 VALU per 192 cells instead of 9 per 128. C5 165.0 -> 159.5 ms;
             // slab 0 of 8 38.6 -> 33.1 ms (its 1041 two-column strips need 261 groups for 256 CUs, and
             // the 5 CUs running two pace the chain; 694 three-column strips fit 174 groups)
-            if (job.ring && job.f2w2 && lin && (g_opt_f2w.load() == 3 || g_opt_f2w.load() == 0) && g_opt_f3.load() != 0 &&
-                g_opt_f3rhl.load() == 0 && (g_opt_C.load() == 0 || g_opt_C.load() == 64)) {
+            if (job.ring && job.f2w2 && (lin ? g_opt_f3.load() != 0 && g_opt_f3rhl.load() == 0 : g_opt_f3a.load() != 0) &&
+                (g_opt_f2w.load() == 3 || g_opt_f2w.load() == 0) && (g_opt_C.load() == 0 || g_opt_C.load() == 64)) {
                 plan_flow2(job, true, false, true);
                 job.ring = true;
             }
@@ -741,7 +741,7 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
         probe.f2_w2 = job.f2w2;
         probe.f3_hl = use_f3 && job.C == 64 && g_opt_f3rhl.load() != 0;
         probe.f3ra = use_f3ra;
-        probe.f3_w3 = use_f3 && job.f2w3;
+        probe.f3_w3 = (use_f3 || use_f3ra) && job.f2w3;
         probe.f3_slab = (use_f3 || use_f3ra) && edge != nullptr;
         if (probe.f3_slab) probe.f3_hl = false;
         int fit = 0;
@@ -825,7 +825,7 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
     // half-chunk links at C = 32, both steps, when option f3pool = 1 (default 0: measured slower)
     cfg.f3p = g_opt_f3pool.load() != 0 && cfg.f3_hl && job.C == 32 && !job.ring && (use_f3 || use_f3a);
     cfg.f3_w3 = job.f2w3;
-    if (job.f2w3 && !(use_f3 && job.ring && job.C == 64 && !cfg.f3_hl)) {
+    if (job.f2w3 && !((use_f3 || use_f3ra) && job.ring && job.C == 64 && !cfg.f3_hl)) {
         set_err("three columns per lane run on flow3's ring kernel only (linear-gap step, C = 64, whole-chunk links)");
         return -1;
     }

@@ -1,8 +1,9 @@
 """GPU parity: three columns per lane in flow3's ring mode (option f2w = 3; sw_flow3.hip
 sw_flow3r3_kernel / sw_flow3r3s_kernel, chunk loops from tools/gen_flow3.py step3): strips of 189
 new columns overlapping by three, the linear-gap step (main.cpp:54-66 at G_INIT == G_EXT, exact,
-DESIGN.md section 2), bit-exact against the oracle (lazySmith.cpp:15-69 restated), against the
-two-column kernel on the same inputs, against the C5 golden, and as column slabs."""
+DESIGN.md section 2) and the affine step (sw_flow3ra3_kernel / sw_flow3ra3s_kernel), bit-exact
+against the oracle (lazySmith.cpp:15-69 restated), against the two-column kernels on the same
+inputs, against the C5 golden, and as column slabs."""
 import numpy as np
 import pytest
 
@@ -118,3 +119,66 @@ def test_w3_slabs(engine, oracle_mod, nslabs):
         assert all(x % 189 == 0 for x in bounds[1:-1]), bounds
         for s in stats:
             assert s["mode"] == 5 and s["variant"] & 8192 and s["variant"] & 2048, s
+
+
+# ---- the affine step at three columns per lane (sw_flow3ra3_kernel / sw_flow3ra3s_kernel,
+# tools/gen_flow3.py step_aff3): G_INIT != G_EXT, or the affine step forced at G_INIT == G_EXT
+
+AFFINE_SETS = ((2, -3, 5, 2), (1, -1, 3, 1), (1, -1, 1, 3))
+
+
+def test_w3_affine_ring_parity(engine, oracle_mod):
+    rng = np.random.default_rng(75)
+    pairs = _pairs(rng)
+    engine.set_option("orient", 1)
+    engine.set_option("mode", 5)
+    engine.set_option("ring", 1)
+    for prm in AFFINE_SETS + ((1, -1, 2, 2),):
+        p = engine.Params(*prm)
+        op = oracle_mod.Params(*prm)
+        engine.set_option("linear", 0 if prm[2] == prm[3] else -1)
+        exp = [oracle_mod.score_linear(a, b, op) for a, b in pairs]
+        for blocks, rows in ((0, 4096), (1, 512), (3, 1024), (7, 512)):
+            engine.set_option("blocks", blocks)
+            engine.set_option("ring_rows", rows)
+            got = []
+            for a, b in pairs:
+                got.append(engine.score(a, b, p))
+                st = engine.last_stats()
+                strips = 1 if len(a) <= 192 else (len(a) - 3 + 188) // 189
+                if strips > 4:
+                    assert st["variant"] & 8192 and st["variant"] & 1024 and st["variant"] & 4, st
+            assert got == exp, (prm, blocks, rows)
+
+
+def test_w3_affine_matches_w2(engine):
+    """A 2^17 pair at (2, -3, 5, 2): three columns per lane give the two-column kernel's score."""
+    a, b = engine.gen_pair(1 << 17, 1 << 17)
+    p = engine.Params(*AFFINE_SETS[0])
+    engine.set_option("ring", 1)
+    engine.set_option("f2w", 2)
+    w2 = engine.score(a, b, p)
+    assert engine.last_stats()["variant"] & 1024 and not engine.last_stats()["variant"] & 8192
+    engine.set_option("f2w", 3)
+    w3 = engine.score(a, b, p)
+    assert engine.last_stats()["variant"] & 8192 and engine.last_stats()["variant"] & 1024
+    assert w3 == w2 > 0
+
+
+@pytest.mark.parametrize("nslabs", [2, 3])
+def test_w3_affine_slabs(engine, oracle_mod, nslabs):
+    rng = np.random.default_rng(77 + nslabs)
+    engine.set_option("ring_rows", 512)
+    engine.set_option("blocks", 3)
+    prm = AFFINE_SETS[0]
+    engine.set_params(engine.Params(*prm))
+    op = oracle_mod.Params(*prm)
+    for n, m in ((nslabs * 2000 + 77, 1500), (nslabs * 1800, 2100)):
+        a = _rand_dna(rng, n)
+        b = _similar(rng, a, m) if m < n else _rand_dna(rng, m)
+        exp = oracle_mod.score_linear(a, b, op)
+        got, bounds, stats = _run_threads(engine, a, b, nslabs, engine.SW_FLAG_DNA)
+        assert max(got) == exp, (n, m, got, exp, bounds)
+        assert all(x % 189 == 0 for x in bounds[1:-1]), bounds
+        for s in stats:
+            assert s["variant"] & 8192 and s["variant"] & 1024 and s["variant"] & 2048, s

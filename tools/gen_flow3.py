@@ -1173,6 +1173,41 @@ def step_aff2(a, b, even):
     a("v_max3_i32 v57, v57, v51, v52")          # M
 
 
+def step_aff3(a, b, even):
+    """One anti-diagonal step of the three-column affine step (25.5 VALU, 192 cells): step_aff2
+    with a column C (v118 H_C, v119 hgOC, v120 fhC, v121 E_C, the flowing E; v122 / v123 tC of
+    even / odd steps, v124 score bytes C); E_B (v50) is a temporary here."""
+    ioh, ioe, l0h, l0e = ("v40", "v41", "v42", "v43") if even else ("v42", "v43", "v40", "v41")
+    tc = "v122" if even else "v123"
+    a(f"v_add_u32_sdwa v51, sext(v55), {l0h} dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_{b} src1_sel:DWORD")
+    a(f"v_add_u32_sdwa v52, sext(v56), v44 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_{b} src1_sel:DWORD")
+    a(f"v_add_u32_sdwa {tc}, sext(v124), v47 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_{b} src1_sel:DWORD")
+    a(f"v_mov_b32_dpp {l0h}, {ioh} wave_shl:1 row_mask:0xf bank_mask:0xf")
+    a(f"v_add_u32_dpp {ioh}, v118, %[ng] wave_shr:1 row_mask:0xf bank_mask:0xf")
+    a(f"v_mov_b32_dpp {l0e}, {ioe} wave_shl:1 row_mask:0xf bank_mask:0xf")
+    a(f"v_add_u32_dpp {ioe}, v121, %[nge] wave_shr:1 row_mask:0xf bank_mask:0xf")
+    a("v_max3_i32 v53, v46, v45, 0")            # F_A
+    a(f"v_max_i32 v54, {ioe}, {ioh}")           # E_A
+    a("v_max3_i32 v44, v51, v54, v53")          # H_A
+    a("v_subrev_u32 v46, %[GE], v53")           # fhA
+    a("v_subrev_u32 v45, %[GI], v44")           # hgOA
+    a("v_subrev_u32 v54, %[GE], v54")           # E_A - GE
+    a("v_max_i32 v50, v54, v45")                # E_B
+    a("v_max3_i32 v53, v49, v48, 0")            # F_B
+    a("v_max3_i32 v47, v52, v50, v53")          # H_B
+    a("v_subrev_u32 v49, %[GE], v53")           # fhB
+    a("v_subrev_u32 v48, %[GI], v47")           # hgOB
+    a("v_subrev_u32 v50, %[GE], v50")           # E_B - GE
+    a("v_max_i32 v121, v50, v48")               # E_C
+    a("v_max3_i32 v53, v120, v119, 0")          # F_C
+    a(f"v_max3_i32 v118, {tc}, v121, v53")      # H_C
+    a("v_subrev_u32 v120, %[GE], v53")          # fhC
+    a("v_subrev_u32 v119, %[GI], v118")         # hgOC
+    a("v_max3_i32 v57, v57, v51, v52")          # M
+    if not even:
+        a("v_max3_i32 v57, v57, v122, v123")
+
+
 def ring_granule_aff(a, key="%[ek]", key2="%[ek2]", cp="sc1"):
     """Publish lanes 32..63 of the I/O pair (the 32 newest outflow rows, row v117) as 16-B
     granules at their ring slots, rows outside [0, m) dropped (peer: slab keys, system scope)."""
@@ -1208,8 +1243,9 @@ def ring_gin_check_aff(a, key="%[ek]", key2="%[ek2]"):
     a("s_cmp_lg_u64 s[50:51], 0")
 
 
-def gen_role_ring_aff(IN, OUT_):
-    """gen_role_ring (C = 64, whole-chunk links) around the two-column affine step."""
+def gen_role_ring_aff(IN, OUT_, W=2):
+    """gen_role_ring (C = 64, whole-chunk links) around the two-column affine step (W = 3: the
+    three-column one, step_aff3)."""
     C = 64
     L = []
     a = L.append
@@ -1220,11 +1256,11 @@ def gen_role_ring_aff(IN, OUT_):
     ncr = C // 16
     a("s_nop 4")
     a("s_waitcnt vmcnt(0) lgkmcnt(0)")
-    for r in ("v44", "v47", "v50", "v57"):
+    for r in ("v44", "v47", "v50", "v57") + (("v118", "v121") if W == 3 else ()):
         a(f"v_mov_b32 {r}, 0")
-    for r in ("v45", "v48", "v40", "v42"):
+    for r in ("v45", "v48", "v40", "v42") + (("v119",) if W == 3 else ()):
         a(f"v_mov_b32 {r}, %[ng]")
-    for r in ("v46", "v49", "v41", "v43"):
+    for r in ("v46", "v49", "v41", "v43") + (("v120",) if W == 3 else ()):
         a(f"v_mov_b32 {r}, %[nge]")
     a("v_mov_b32 v101, %[raw2]")
     a("v_mov_b32 v115, %[cro]")
@@ -1344,8 +1380,10 @@ def gen_role_ring_aff(IN, OUT_):
         for u in range(C // 4):
             a(f"v_perm_b32 v55, %[pA], %[k80], v{cur + u}")
             a(f"v_perm_b32 v56, %[pB], %[k80], v{cur + u}")
+            if W == 3:
+                a(f"v_perm_b32 v124, %[pC], %[k80], v{cur + u}")
             for b in range(4):
-                step_aff2(a, b, b % 2 == 0)
+                (step_aff3 if W == 3 else step_aff2)(a, b, b % 2 == 0)
             if gout and u == 7:
                 ring_granule_aff(a, *kout)
         a(f"s_add_i32 s40, s40, {C}")
@@ -1442,19 +1480,32 @@ OUT_RING_AFF = os.path.join(ROOT, "concurrentproject_amd", "csrc", "sw_flow3ra_l
 
 def emit_ring_aff():
     out = ["// GENERATED by tools/gen_flow3.py -- do not edit.  The flow3 ring-mode affine-step chunk loops",
-           "// (sw_flow3.hip sw_flow3ra_kernel): one inline-asm block per strip role, C = 64, R = %d rows of 8-B slots." % RR,
+           "// (sw_flow3.hip sw_flow3ra_kernel): one inline-asm block per strip role, C = 64, R = %d rows of 8-B slots;" % RR,
+           "// f3ra3_loop: three columns per lane (step_aff3), ALN = 1 the s_nop-aligned ones of the column-slab kernel.",
            "// Operands: see F3RALoop in sw_flow3.hip; fixed registers: tools/gen_flow3.py (gen_role_ring_aff).",
            "#pragma once", ""]
-    for IN, OUT_ in [(i, o) for i in ROLES_IN_RING for o in ROLES_OUT] + list(ROLES_SLAB):
-        body = align8(gen_role_ring_aff(IN, OUT_), nops=RING_NOPS) if RING_ALIGN else gen_role_ring_aff(IN, OUT_)
-        out.append("template <> __device__ __forceinline__ F3Res f3ra_loop<F3_%s, F3_%s>(const F3RALoop& x) {"
-                   % (IN.upper(), OUT_.upper()))
+    ring_roles = [(i, o) for i in ROLES_IN_RING for o in ROLES_OUT]
+    combos = [(i, o, 2, 0) for i, o in ring_roles + list(ROLES_SLAB)] + \
+        [(i, o, 3, 0) for i, o in ring_roles] + [(i, o, 3, 1) for i, o in ring_roles + list(ROLES_SLAB)]
+    for IN, OUT_, W, aln in combos:
+        body = gen_role_ring_aff(IN, OUT_, W)
+        if W == 2 and RING_ALIGN:
+            body = align8(body, nops=RING_NOPS)
+        if aln:
+            body = align8(body, nops=True, promote=False)
+        if W == 2:
+            out.append("template <> __device__ __forceinline__ F3Res f3ra_loop<F3_%s, F3_%s>(const F3RALoop& x) {"
+                       % (IN.upper(), OUT_.upper()))
+        else:
+            out.append("template <> __device__ __forceinline__ F3Res f3ra3_loop<F3_%s, F3_%s, %d>(const F3RALoop& x) {"
+                       % (IN.upper(), OUT_.upper(), aln))
         out.append("    F3Res r;")
         out.append("    asm volatile(")
         for line in body:
             out.append('        "%s\\n\\t"' % line)
         out.append('        : [M] "=v"(r.M), [fail] "=s"(r.fail), [slow] "=s"(r.slow)')
-        out.append('        : [pA] "v"(x.pA), [pB] "v"(x.pB), [ng] "v"(x.ng), [nge] "v"(x.nge), [GI] "s"(x.GI),')
+        out.append('        : [pA] "v"(x.pA), [pB] "v"(x.pB), [ng] "v"(x.ng), [nge] "v"(x.nge), [GI] "s"(x.GI),' if W == 2 else
+                   '        : [pA] "v"(x.pA), [pB] "v"(x.pB), [pC] "v"(x.pC), [ng] "v"(x.ng), [nge] "v"(x.nge), [GI] "s"(x.GI),')
         out.append('          [GE] "s"(x.GE), [k80] "s"(x.k80), [m] "s"(x.m), [end] "s"(x.end), [dlo] "s"(x.dlo),')
         out.append('          [dhi] "s"(x.dhi), [lane] "v"(x.lane), [raw2] "v"(x.raw2), [cro] "v"(x.cro), [c0] "v"(x.c0),')
         out.append('          [cbase] "v"(x.cbase), [cwr] "v"(x.cwr), [cwm] "v"(x.cwm), [rrs] "s"(x.rrs), [rrow] "v"(x.rrow),')
@@ -1465,7 +1516,8 @@ def emit_ring_aff():
         out.append('          [gors] "s"(x.gors), [gooff] "v"(x.gooff), [gopos] "v"(x.gopos), [gomask16] "s"(x.gomask16),')
         out.append('          [gorow] "v"(x.gorow), [lhi] "s"(x.lhi), [bpr] "s"(x.bpr), [bpbase] "s"(x.bpbase),')
         out.append('          [ekp] "s"(x.ekp), [ek2p] "s"(x.ek2p)')
-        out.append("        : " + ", ".join(CLOBBERS_RING_AFF) + ");")
+        clob = CLOBBERS_RING_AFF + (['"v%d"' % r for r in range(118, 125)] if W == 3 else [])
+        out.append("        : " + ", ".join(clob) + ");")
         out.append("    return r;")
         out.append("}")
         out.append("")
