@@ -65,7 +65,7 @@ Params g_params;
 std::atomic<long long> g_opt_W{0}, g_opt_C{0}, g_opt_bytes{0}, g_opt_timeout{30}, g_opt_blocks{0}, g_opt_orient{0},
     g_opt_mode{-1}, g_opt_trace{0}, g_opt_duo_f16{1}, g_opt_f2stream{0}, g_opt_ring{-1}, g_opt_ring_rows{4096}, g_opt_f2_wgs{0}, g_opt_f2w{0}, g_opt_f2pwg{-1},
     g_opt_linear{-1}, g_opt_f3{1}, g_opt_slab_plain{0}, g_opt_duo_lds{1}, g_opt_duo_tab{1}, g_opt_duo_roles{1}, g_opt_f3hl{1},
-    g_opt_f3rhl{0}, g_opt_f3a{1}, g_opt_f3slab{1}, g_opt_duo_prio{0}, g_opt_f3pool{0};
+    g_opt_f3rhl{0}, g_opt_f3a{1}, g_opt_f3slab{1}, g_opt_duo_prio{-1}, g_opt_f3pool{0};
 
 // Longest sequence the engine takes: granule buffers of m rows keep m * 16 in the
 // 32-bit record count of a buffer resource (sw_device.h linear_edge).
@@ -896,7 +896,11 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
     if (duo_wrap > 0) {
         kp.wrap_rows = duo_wrap;
         if (g_opt_duo_roles.load() != 0) kp.ring_cons = c->cons.p;   // per-CU role words (zeroed above)
-        kp.duo_prio = (int)g_opt_duo_prio.load();
+        // auto (-1): turn-taking in 1.3 ms slices for one-pass batches (LDS table: one duo per workgroup,
+        // the CU's two workgroups would otherwise end ~3 ms apart, C3 6.48 -> 6.30 ms); off for longer
+        // batches (C4 51.3 -> 51.6 ms with it), profiles/r05_duo_prio.md
+        const int dp = (int)g_opt_duo_prio.load();
+        kp.duo_prio = dp >= 0 ? dp : cfg.duo_tab > 0 ? 17 : 0;
     }
     kp.timeout_ticks = g_opt_timeout.load() * 100000000LL;   // s_memrealtime: 100 MHz
     kp.trace = reinterpret_cast<unsigned long long*>(g_opt_trace.load());
@@ -1755,8 +1759,8 @@ int sw_set_option(const char* key, long long v) {
     } else if (k == "f3rhl") {   // 1: flow3 ring launches at C = 64 with half-chunk in-workgroup links
         if (v < 0 || v > 1) return -1;
         g_opt_f3rhl = v;
-    } else if (k == "duo_prio") {   // duo LDS kernel: 0 off, k > 0 workgroups of a CU alternate priority every 2^(k-1) chunks
-        if (v < 0 || v > 8) return -1;
+    } else if (k == "duo_prio") {   // duo LDS kernel: -1 auto, 0 off, k in 6..20: workgroups of a CU alternate priority every 2^k clock ticks (10 ns)
+        if (v != 0 && v != -1 && (v < 6 || v > 20)) return -1;
         g_opt_duo_prio = v;
     } else if (k == "f3slab") {   // 1 (default): column slabs on flow3's ring kernel (sw_flow3rs_kernel), 0: flow2
         if (v < 0 || v > 1) return -1;

@@ -97,8 +97,8 @@ struct KParams {
     int wrap_rows;
     unsigned* ring_cons;          // ring j's consumer progress (positions consumed), RING_CONS_STRIDE apart;
                                   // duo LDS kernel: DUO_CU_WORDS zeroed role words (or null)
-    int duo_prio;                 // duo LDS kernel with roles: 0 = off, k > 0 = the CU's two workgroups
-                                  // take turns at issue priority every 2^(k-1) chunks (s_setprio)
+    int duo_prio;                 // duo LDS kernel with roles: 0 = off, k in 6..20 = the CU's two workgroups
+                                  // take turns at issue priority every 2^k ticks of s_memrealtime (s_setprio)
     // (the duo kernel with LDS hand-offs takes its wrap-buffer slots from wrap_rows)
 };
 

@@ -1114,7 +1114,8 @@ __device__ void strip_pass_duo_lds(const KParams& kp, const DuoDesc& d, const in
                                    const bool has_in, const DuoLink<LIN> in, const bool has_out,
                                    const DuoLink<LIN> out, int* const prod_out, int* const cons_out,
                                    DuoSlot<LIN>* const sink, unsigned* const tab, const bool build,
-                                   int* const ready_out, const int ready_val, const int prio_par) {
+                                   int* const ready_out, const int ready_val, const int prio_par,
+                                   const long long prio_t0) {
     constexpr int SW = 64 * W;
     static_assert(C == 64, "the LDS links move one row per lane and chunk");
     const int m = d.m_pad;
@@ -1150,15 +1151,19 @@ __device__ void strip_pass_duo_lds(const KParams& kp, const DuoDesc& d, const in
     [[maybe_unused]] int spin_n = 0;   // polls (spin_expired)
     bool failed = false;
     int cons_seen = 0;
+    long long prio_t = t_start;   // the clock read one chunk ago (kp.duo_prio)
     for (int c = 0; c < nchunks; ++c) {
         const int k0 = c * C;
         const unsigned raw0 = raw0_nxt, raw1 = raw1_nxt;
-        // kp.duo_prio: the CU's two workgroups (prio_par 0 / 1) take turns at issue priority, so
-        // neither runs alone on its SIMDs at the end (old-wave-first arbitration otherwise lets
-        // the first one finish far ahead: wave end times at ~3.2 and ~6.4 ms on C3)
+        // kp.duo_prio = k: the CU's two workgroups (prio_par 0 / 1) take turns at issue priority in
+        // slices of 2^k ticks of the 100 MHz clock from their start (the second-placed one first), so
+        // neither runs alone on its SIMDs at the end: old-wave-first arbitration otherwise lets the
+        // first one finish at ~3.4 ms and the second at ~6.4 on C3; at k = 17 both end at ~6.0-6.3
+        // (profiles/r05_duo_prio.md). Slices under ~0.3 ms do not balance them.
         if (prio_par >= 0) {
-            if ((((unsigned)c >> (kp.duo_prio - 1)) ^ (unsigned)prio_par) & 1u) __builtin_amdgcn_s_setprio(2);
+            if ((((unsigned long long)(prio_t - prio_t0) >> kp.duo_prio) ^ (unsigned)prio_par) & 1u) __builtin_amdgcn_s_setprio(2);
             else __builtin_amdgcn_s_setprio(0);
+            prio_t = (long long)__builtin_amdgcn_s_memrealtime();
         }
         if constexpr (TAB) {
             if (build) {   // table rows k0 + 128 .. k0 + 191 (bytes loaded a chunk ago), bytes of the next 64
@@ -1349,7 +1354,7 @@ __global__ void __launch_bounds__(64 * DUO_WAVES) sw_duo_lds_kernel(KParams kp) 
                                        wave < 3 ? base : 0, base, nullptr, wave < 3 ? &cons[wave + 1] : nullptr};
                 strip_pass_duo_lds<W, C, M3, LIN, TAB>(kp, d, strip, lane, strip > 0, in, strip + 1 < d.strips, out,
                                                        prod_out, cons_out, sink[wave], tab, strip == 0, ready_out,
-                                                       dseq + 1, prio_par);
+                                                       dseq + 1, prio_par, t_begin);
             }
             // done with every position before the next round, read or not: a producer's back-pressure
             // must not wait on a consumer that skipped rounds (idle waves of a duo's last round) --

@@ -64,6 +64,13 @@ def test_options_host_side():
     with pytest.raises(sw.SwError):
         sw.set_option("nope", 1)
     sw.set_option("W", 0); sw.set_option("C", 0); sw.set_option("timeout", 30)
+    assert sw.get_option("duo_prio") == -1               # auto: turn-taking on the LDS-table duo kernel
+    for v in (0, 6, 17, 20, -1):
+        sw.set_option("duo_prio", v)
+        assert sw.get_option("duo_prio") == v
+    for bad in (-2, 1, 5, 21):
+        with pytest.raises(sw.SwError):
+            sw.set_option("duo_prio", bad)
 
 
 def test_slab_bounds_host_side():

@@ -136,3 +136,24 @@ def test_duo_lds_c3_golden(engine, golden):
             assert got == c["scores"], (tab, roles)
     finally:
         engine.set_option("duo_roles", 1)
+
+
+def test_duo_lds_priority_turns(engine, golden):
+    """Turn-taking at issue priority between a CU's two workgroups (option duo_prio: -1 auto = 1.3 ms
+    slices on the LDS-table kernel, 0 off, short and long slices) changes timing only: C3 scores
+    equal the golden under each; out-of-range values are refused."""
+    c = golden("configs.json")["C3"]
+    N = c["N"]
+    arena = engine.gen_batch(c["seed_base"], c["npairs"], N)
+    pairs = [(arena[2 * N * k:2 * N * k + N], arena[2 * N * k + N:2 * N * (k + 1)]) for k in range(c["npairs"])]
+    try:
+        for k in (-1, 0, 6, 17):
+            engine.set_option("duo_prio", k)
+            assert engine.get_option("duo_prio") == k
+            assert engine.score_batch(pairs) == c["scores"], k
+            assert engine.last_stats()["variant"] & 256
+        for bad in (-2, 1, 5, 21):
+            with pytest.raises(engine.SwError):
+                engine.set_option("duo_prio", bad)
+    finally:
+        engine.set_option("duo_prio", -1)

@@ -4,7 +4,7 @@ option; per wave HW_ID (SIMD, CU, SH, SE), XCC_ID, begin and end (s_memrealtime,
 Prints how strip roles map to SIMDs on the CUs that hold two workgroups, and the per-SIMD
 idle time at the start and end of the launch.
 
-    python tools/probe_duo_simd.py [duo_tab]
+    python tools/probe_duo_simd.py [duo_tab [duo_prio]]
 """
 import collections
 import os
@@ -26,6 +26,8 @@ def main():
     offs_a = [2 * N * k for k in range(P)]
     offs_b = [2 * N * k + N for k in range(P)]
     sw.set_option("duo_tab", rev)
+    if len(sys.argv) > 2:
+        sw.set_option("duo_prio", int(sys.argv[2]))
     s = torch.cuda.current_stream()
     trace = None
     for it in range(3):
@@ -74,6 +76,10 @@ def main():
     ends = sorted(end)
     print("end us: min %.1f median %.1f max %.1f; SIMD idle at the end: median %.1f us" %
           (ends[0], ends[len(ends) // 2], ends[-1], float(np.median(idle_end))))
+    wg_end = [sorted(e for _, e in v) for v in by_cu.values() if len(v) == 2]
+    if wg_end:
+        print("workgroup end per CU: first median %.1f us, second median %.1f us" %
+              (float(np.median([w[0] for w in wg_end])), float(np.median([w[1] for w in wg_end]))))
     for r in range(4):
         sel = role == r
         print("role %d: end median %.1f us" % (r, float(np.median(end[sel]))))
