@@ -612,6 +612,10 @@ def main():
         sys.exit("bench.py: rank %d needs GPU %d, this host shows %d" % (rank, local, visible_devices()))
     import torch
     torch.cuda.set_device(local)
+    # launches go on a stream of their own: on torch's default stream cuda_stream is 0, and
+    # sw_score_batch_device then runs its blocking form (a stream sync and error check per call,
+    # the GPU idle while the host plans the next one: 0.35 ms a C3 step, profiles/r05_c3_hip_trace.md)
+    torch.cuda.set_stream(torch.cuda.Stream())
     dist = None
     rccl = None
     if world > 1 or launcher_env():
