@@ -217,6 +217,9 @@ void sw_db_close(sw_db* db);
  *              columns per lane, when the table and the wrap buffer fit two workgroups per CU
  *              and the duos run in one pass at that), 2 = whenever it fits, 0 = the codes travel
  *              lane to lane by DPP
+ *   "duo_prio" -1 = (default) auto: 17 for the duo LDS kernel with the row-code table, else 0;
+ *              k in 6..20: a CU's two duo workgroups take turns at issue priority (s_setprio) in
+ *              slices of 2^k ticks (10 ns) of the clock from their start; 0 = off (timing only)
  *   "slab_plain" 1 = an exported slab buffer may fall back to plain device memory (one-GPU
  *              tests only; cross-GPU edges need fine-grained memory), 0 = (default) refuse
  *   "trace"    device address of a 16 x u64 per-strip trace buffer, 0 = off (tools)
