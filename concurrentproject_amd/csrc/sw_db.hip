@@ -76,6 +76,12 @@ int device_arena(sw_db* db, int qlen, sw_db::Dev** out) {
     return 0;
 }
 
+bool all_dna(const unsigned char* p, size_t n) {
+    unsigned bad = 0;
+    for (size_t i = 0; i < n; ++i) bad |= !(p[i] == 'A' || p[i] == 'C' || p[i] == 'G' || p[i] == 'T');
+    return bad == 0;
+}
+
 // qslot: room to reserve for the query (>= qlen; a query database sizes it once
 // for its longest query, so the residue arena is uploaded once)
 int search(sw_db* db, const unsigned char* query, int qlen, int* scores_out, int qslot) {
@@ -103,7 +109,11 @@ int search(sw_db* db, const unsigned char* query, int qlen, int* scores_out, int
         b_off[k] = db->off[r];
         blen[k] = db->len[r];
     }
-    if (sw_score_batch_device(v->arena, a_off.data(), alen.data(), b_off.data(), blen.data(), nrec, v->scores, 0,
+    // the alphabet the engine would scan for on the device (its alphabet_kernel), known on the host:
+    // the records' once per database, the query's per search
+    if (db->dna < 0) db->dna = all_dna(db->res.data(), db->res.size()) ? 1 : 0;
+    const int flags = db->dna == 1 && all_dna(query, (size_t)qlen) ? SW_FLAG_DNA : SW_FLAG_BYTES;
+    if (sw_score_batch_device(v->arena, a_off.data(), alen.data(), b_off.data(), blen.data(), nrec, v->scores, flags,
                               nullptr))
         return -1;
     std::vector<int> got((size_t)nrec);

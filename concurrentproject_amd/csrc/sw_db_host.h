@@ -16,6 +16,7 @@ struct sw_db {
     std::vector<int> len;
     std::vector<std::string> header;    // the '>' line without '>' and line end
     std::vector<int> order;             // record indices, longest first
+    int dna = -1;                       // every residue in {A,C,G,T}: 1 / 0, -1 not scanned yet (sw_db.hip)
     struct Dev {
         unsigned char* arena = nullptr; // residues, then qcap bytes of query slot
         size_t qcap = 0;

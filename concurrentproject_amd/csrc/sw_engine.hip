@@ -304,10 +304,12 @@ bool duo_f16_fits(const Job& job, const Params& p) {
 void plan_duos(Job& job) {
     std::vector<int> ord(job.pairs.size());
     for (size_t i = 0; i < ord.size(); ++i) ord[i] = (int)i;
-    std::sort(ord.begin(), ord.end(), [&](int x, int y) {
+    const auto by_shape = [&](int x, int y) {
         const PairDesc &a = job.pairs[x], &b = job.pairs[y];
         return a.n != b.n ? a.n > b.n : a.m > b.m;
-    });
+    };
+    // callers that pass pairs in shape order already (sw_db: records longest first) skip the sort
+    if (!std::is_sorted(ord.begin(), ord.end(), by_shape)) std::sort(ord.begin(), ord.end(), by_shape);
     job.duos.clear();
     uint64_t g = 0;
     for (size_t i = 0; i < ord.size(); i += 2) {
