@@ -712,8 +712,11 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
     // duo batches at C = 64: strip hand-offs in LDS when the wrap buffer (a round's rows of
     // both pairs) fits the default dynamic-LDS limit; no boundary buffers in HBM then
     // and, at 4 or 8 columns per lane, the row codes from an LDS table when both fit two workgroups per CU
-    // and the duos run in one pass at that (C3, 512 duos: 6.80 -> 6.54 ms); more duos keep the table-less
-    // kernel, whose smaller LDS admits 4 per CU (8192 pairs of 8192: 51.3 ms against 52.0 with the table)
+    // and the duos run in one pass at that (C3, 512 duos: 6.80 -> 6.54 ms), or rows are 8192 or more; more
+    // duos of shorter rows keep the table-less kernel, whose smaller LDS admits 4 per CU. With the CU's two
+    // workgroups taking turns at priority (duo_prio) the table wins at 8192 rows: 8192 pairs of 8192
+    // 51.8 -> 50.5 ms, 2048 pairs 13.2 -> 12.6, 4096 pairs of 1024 x 8192 4.59 -> 4.46; it loses at 4096 rows
+    // (4096 pairs of 4096: 7.88 -> 8.03) and on the ragged DB search (17.9 -> 19.7), r05_duo_prio.md
     int duo_wrap = 0, duo_tab = 0;
     if (duo && job.C == 64 && g_opt_duo_lds.load() != 0) {
         int max_mp = 0;
@@ -721,7 +724,7 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
         const int slots = duo_wrap_slots(max_mp);
         const long long wrap_b = (long long)slots * (f2_lin ? 4 : 8);
         const int tab_w = DUO_TAB_OFF + max_mp + DUO_TAB_TAIL;
-        const bool one_pass = (long long)job.duos.size() <= 2LL * c->cus || g_opt_duo_tab.load() == 2;
+        const bool one_pass = (long long)job.duos.size() <= 2LL * c->cus || g_opt_duo_tab.load() == 2 || max_mp >= 8192;
         if (g_opt_duo_tab.load() != 0 && one_pass && job.W % 4 == 0 && wrap_b + 4LL * tab_w + 16 <= duo_lds_fit(f2_lin)) {
             duo_wrap = slots;
             duo_tab = tab_w;

@@ -4,7 +4,7 @@ Times ``Database.search`` (sw_db_search, synchronous: query H2D + one batch laun
 so the figure is host-API GCUPS, not kernel-only.  Records are uniform ACGT with lengths drawn uniformly from
 [lo, hi]; the arena is uploaded to HBM by the first (untimed) search.
 
-    python tools/bench_db.py [--records R] [--qlen Q] [--lo L] [--hi H] [--steps K]
+    python tools/bench_db.py [--records R] [--qlen Q] [--lo L] [--hi H] [--steps K] [--opt k=v ...]
 """
 import argparse
 import json
@@ -25,7 +25,12 @@ def main():
     ap.add_argument("--lo", type=int, default=256)
     ap.add_argument("--hi", type=int, default=4096)
     ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--opt", action="append", default=[], help="engine option k=v (sw_set_option), repeatable")
     a = ap.parse_args()
+    import concurrentproject_amd as sw
+    for kv in a.opt:
+        k, v = kv.split("=")
+        sw.set_option(k, int(v))
     rng = np.random.default_rng(4)
     acgt = np.frombuffer(b"ACGT", dtype=np.uint8)
     lens = rng.integers(a.lo, a.hi + 1, size=a.records)
