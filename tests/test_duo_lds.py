@@ -157,3 +157,32 @@ def test_duo_lds_priority_turns(engine, golden):
                 engine.set_option("duo_prio", bad)
     finally:
         engine.set_option("duo_prio", -1)
+
+
+def test_duo_lds_table_multi_pass_long_rows(engine, oracle_mod):
+    """Batches of more duos than two per CU take the LDS-table kernel when their rows reach 8192 (the
+    table is rewritten per duo, workgroups taking turns at priority): 1100 pairs of 8192 rows x 64..320
+    columns, against the table-less kernel (duo_tab = 0) and the oracle on a sample."""
+    rng = np.random.default_rng(21)
+    pairs = []
+    for k in range(1100):
+        n = int(rng.integers(64, 321))
+        pairs.append(_related(rng, n, 8192) if k % 2 else (_rand_dna(rng, n), _rand_dna(rng, 8192)))
+    engine.set_option("orient", 1)
+    engine.set_option("mode", 3)
+    engine.set_option("W", 8)
+    engine.set_option("C", 64)
+    try:
+        engine.set_option("duo_tab", 1)
+        tab = engine.score_batch(pairs)
+        st = engine.last_stats()
+        assert st["mode"] == 3 and st["variant"] & 128 and st["variant"] & 256 and st["items"] == 550, st
+        engine.set_option("duo_tab", 0)
+        plain = engine.score_batch(pairs)
+        assert not engine.last_stats()["variant"] & 256
+        assert tab == plain
+        op = oracle_mod.Params(1, -1, 1, 1)
+        for k in range(0, 1100, 157):
+            assert tab[k] == oracle_mod.score_linear(pairs[k][0], pairs[k][1], op), k
+    finally:
+        engine.set_option("orient", 0)
