@@ -330,6 +330,41 @@ def affine_runs(sw, torch, launch, scores, stream, gold, N, steps, params, defau
     return out
 
 
+def batch_affine_runs(sw, torch, gold, steps, params, cells):
+    """N = 1 extras of the batched workload: C3 (1024 pairs N = 8192, seeds 8192 + k) with the
+    general Gotoh step at AFFINE_PARAMS, on the automatic plan (the packed-u16 duo kernel) and on
+    the int32 pair-per-workgroup kernel, each against the reference-pinned golden C3_affine."""
+    ref = gold.get("C3_affine", {}).get("scores", [])
+    out = {}
+    sw.set_params(sw.Params(*AFFINE_PARAMS))
+    try:
+        bt, bk, bsc, bcells, bst = run_batch(sw, torch, None, 1, 0, 8192, 1024, steps, 1)
+        out = {"params": list(AFFINE_PARAMS), "workload": "C3 batch of 1024 pairs N=8192 (seeds 8192+k)",
+               "value": round(bcells * steps / bt / 1e9, 3), "unit": "GCUPS",
+               "ms_per_step": round(bt / steps * 1e3, 4), "kernel_ms_per_launch": round(bk, 4),
+               "kernel_gcups": round(bcells / (bk * 1e-3) / 1e9, 3),
+               "parity": ("ok" if bsc == ref else "MISMATCH") if len(ref) == 1024 else "unchecked",
+               "golden": "C3_affine (all 1024 pairs, reference LazySmith built with these constants)",
+               **kernel_label(bst),
+               "dtype": "u16x2 (packed, exact: scores < 2^16)" if bst["mode"] == 3 else "int32",
+               "roofline": roofline("batch" + affine_key(bst), bcells, bk,
+                                    waves_per_simd=resident_waves_per_simd(bst, torch))}
+        sw.set_option("mode", 5)
+        sw.set_option("f2pwg", 1)
+        try:
+            it, ik, isc, _, ist = run_batch(sw, torch, None, 1, 0, 8192, 1024, 2, 1)
+            out["int32_kernel"] = {"kernel_ms_per_launch": round(ik, 4),
+                                   "kernel_gcups": round(bcells / (ik * 1e-3) / 1e9, 3),
+                                   "parity": ("ok" if isc == ref else "MISMATCH") if len(ref) == 1024 else "unchecked",
+                                   **kernel_label(ist)}
+        finally:
+            sw.set_option("mode", -1)
+            sw.set_option("f2pwg", -1)
+    finally:
+        sw.set_params(sw.Params(*params))
+    return out
+
+
 def c5_runs(sw, torch, gold, steps):
     """N = 1 extras: config C5 (one pair N = 2^20, seed 1048576, O(N) device state) with the
     reference's constants and with AFFINE_PARAMS, each against its golden."""
@@ -364,9 +399,9 @@ def c5_runs(sw, torch, gold, steps):
 
 
 def affine_key(st):
-    """"_affine" when a single-pair launch ran the general affine step (its counter profile is
-    profiles/pmc_<workload>_affine.json, tools/pmc_summary.py c2a / c5a)."""
-    return "_affine" if st["mode"] == 5 and not st["variant"] & 8 else ""
+    """"_affine" when a launch ran the general affine step (its counter profile is
+    profiles/pmc_<workload>_affine.json, tools/pmc_summary.py c2a / c3a / c5a)."""
+    return "_affine" if st["mode"] in (3, 5) and not st["variant"] & 8 else ""
 
 
 def flow2_strips(n, w2=False):
@@ -663,6 +698,10 @@ def main():
             ref = gold.get("C4", gold.get("C3", {})).get("scores", [])
             if len(ref) >= len(allsc):
                 parity = "ok" if allsc == ref[:len(allsc)] else "MISMATCH"
+        elif rank == 0 and params == AFFINE_PARAMS and N == 8192 and world == 1:
+            ref = gold.get("C3_affine", {}).get("scores", [])
+            if len(ref) == len(allsc):
+                parity = "ok" if allsc == ref else "MISMATCH"
     else:
         slabs, slab_buf, slab_cols = None, None, None
         if workload == "pair":
@@ -804,6 +843,8 @@ def main():
                 finally:
                     sw.set_option("mode", args.mode if args.mode >= 0 else -1)
                     sw.set_option("f2pwg", -1)
+            if defaults and args.mode < 0:
+                extra["affine_step"] = batch_affine_runs(sw, torch, gold, bsteps, params, bcells)
 
     value = cells_job * args.steps / t_max / 1e9
     if rank == 0:

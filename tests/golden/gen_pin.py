@@ -16,6 +16,13 @@ TEST INFRASTRUCTURE (build container only: it needs oracle/_ref, compiled in pla
               C3_affine.
   --similar   the same at C2 size on oracle.similar_pair(7, 65536) (long alignments, long gaps),
               as configs.json C2_affine_similar.
+  --c3similar  C3's shape with long E/F legs: oracle.similar_pair(8192 + k, 8192), k < --npairs,
+              at (2, -3, 5, 2), by the reference's refvar LazySmith and swo_linear, as
+              configs.json C3_affine_similar.
+  --c5similar ENGINE  oracle.similar_pair(20, 2^20) at (2, -3, 5, 2) (the C5-size E/F-heavy pair),
+              ENGINE "ref" or "wavefront" as for --c5affine; writes
+              tests/golden/c5_affine_similar_<engine>.json; --merge-c5 also writes
+              configs.json C5_affine_similar when the results present agree.
   --c5affine ENGINE   the C5 pair (seed 1048576, N = 2^20) at (2, -3, 5, 2): ENGINE "ref" (the
               reference's LazySmith refvar build, 1 thread, hours) or "wavefront" (the oracle's
               pthread restatement); writes tests/golden/c5_affine_<engine>.json; --merge-c5 then
@@ -125,8 +132,43 @@ def pin_similar() -> None:
     print("C2_affine_similar", r, round(t_ref, 1), flush=True)
 
 
-def c5_affine(engine: str, threads: int) -> None:
-    a, b = oracle.gen_pair(1048576, 1 << 20)
+def pin_c3_similar(threads: int, npairs: int) -> None:
+    fn = ref_lazy(AFF)
+
+    def one_ref(k):
+        a, b = oracle.similar_pair(8192 + k, 8192)
+        return fn(a, b)
+
+    def one_oracle(k):
+        a, b = oracle.similar_pair(8192 + k, 8192)
+        return oracle.score_linear(a, b, AFF)
+
+    t0 = time.time()
+    with ThreadPoolExecutor(threads) as ex:
+        sc = list(ex.map(one_ref, range(npairs)))
+    t_ref = time.time() - t0
+    with ThreadPoolExecutor(threads) as ex:
+        so = list(ex.map(one_oracle, range(npairs)))
+    assert sc == so, [k for k in range(npairs) if sc[k] != so[k]][:8]
+    cfg = json.load(open(PATH))
+    cfg["C3_affine_similar"] = {
+        "generator": "oracle.similar_pair(8192 + k, 8192), k < npairs", "seed_base": 8192, "N": 8192,
+        "npairs": npairs, "params": [AFF.match, AFF.mismatch, AFF.gap_init, AFF.gap_ext], "scores": sc,
+        "pinned_by": ["reference LazySmith built with (2,-3,5,2) (oracle/Makefile refvar), "
+                      "%d threads, %.0f s (tests/golden/gen_pin.py --c3similar)" % (threads, t_ref),
+                      "oracle swo_linear"]}
+    json.dump(cfg, open(PATH, "w"), indent=1)
+    print("C3_affine_similar", sc[:8], min(sc), max(sc), round(t_ref, 1), flush=True)
+
+
+C5_SIMILAR_SEED = 20
+
+
+def c5_affine(engine: str, threads: int, similar: bool = False) -> None:
+    if similar:
+        a, b = oracle.similar_pair(C5_SIMILAR_SEED, 1 << 20)
+    else:
+        a, b = oracle.gen_pair(1048576, 1 << 20)
     t0 = time.time()
     if engine == "ref":
         s = ref_lazy(AFF)(a, b)
@@ -136,8 +178,27 @@ def c5_affine(engine: str, threads: int) -> None:
         src = "oracle swo_wavefront (sw_oracle.c, main.cpp:54-66 restated), %d threads" % threads
     out = {"seed": 1048576, "N": 1 << 20, "params": [AFF.match, AFF.mismatch, AFF.gap_init, AFF.gap_ext],
            "score": int(s), "seconds": round(time.time() - t0, 1), "sha256": sha(a, b), "source": src}
-    json.dump(out, open(os.path.join(HERE, "c5_affine_%s.json" % engine), "w"), indent=1)
+    name = "c5_affine_%s.json" % engine
+    if similar:
+        del out["seed"]
+        out["generator"] = "oracle.similar_pair(%d, 2^20)" % C5_SIMILAR_SEED
+        name = "c5_affine_similar_%s.json" % engine
+    json.dump(out, open(os.path.join(HERE, name), "w"), indent=1)
     print(json.dumps(out), flush=True)
+
+
+def merge_c5_similar() -> None:
+    res = [json.load(open(os.path.join(HERE, "c5_affine_similar_%s.json" % e))) for e in ("ref", "wavefront")
+           if os.path.exists(os.path.join(HERE, "c5_affine_similar_%s.json" % e))]
+    if not res:
+        return
+    assert len({r["score"] for r in res}) == 1 and len({r["sha256"] for r in res}) == 1
+    cfg = json.load(open(PATH))
+    cfg["C5_affine_similar"] = {"generator": res[0]["generator"], "N": 1 << 20, "params": res[0]["params"],
+                                "score": res[0]["score"], "sha256": res[0]["sha256"],
+                                "pinned_by": [r["source"] + " in %.0f s" % r["seconds"] for r in res]}
+    json.dump(cfg, open(PATH, "w"), indent=1)
+    print("C5_affine_similar", cfg["C5_affine_similar"])
 
 
 def merge_c5() -> None:
@@ -161,13 +222,20 @@ if __name__ == "__main__":
     ap.add_argument("--similar", action="store_true")
     ap.add_argument("--c5affine", choices=["ref", "wavefront"])
     ap.add_argument("--merge-c5", action="store_true")
+    ap.add_argument("--c3similar", action="store_true")
+    ap.add_argument("--c5similar", choices=["ref", "wavefront"])
     args = ap.parse_args()
     if args.similar:
         pin_similar()
     if args.c5affine:
         c5_affine(args.c5affine, args.threads)
+    if args.c5similar:
+        c5_affine(args.c5similar, args.threads, similar=True)
     if args.merge_c5:
         merge_c5()
+        merge_c5_similar()
+    if args.c3similar:
+        pin_c3_similar(args.threads, args.npairs)
     if args.affine:
         pin_affine(args.threads, args.npairs)
     if args.c4:

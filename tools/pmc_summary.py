@@ -2,7 +2,7 @@
 """Turn the rocprofv3 passes written by tools/prof_round.sh into the committed
 profile summaries.
 
-    python tools/pmc_summary.py gpurun_out/prof r02
+    python tools/pmc_summary.py gpurun_out/prof r02 [c2,c3a,...]
 
 For each workload (c2 -> pair, c3 -> batch, c5 -> slab on one GPU, c5p8 -> slab_part: slab 0 of
 C5's 8-way column split alone):
@@ -38,9 +38,10 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ALGO_BYTES_PER_CELL = 12
 CELLS = {"c2": 65536 * 65536, "c3": 1024 * 8192 * 8192, "c5": (1 << 20) * (1 << 20),
-         "c2a": 65536 * 65536, "c5a": (1 << 20) * (1 << 20)}
-# c2a / c5a: the same pairs with the affine constants (2, -3, 5, 2) (bench.py AFFINE_PARAMS)
-WORKLOAD = {"c2": "pair", "c3": "batch", "c5": "slab", "c5p8": "slab_part", "c2a": "pair_affine", "c5a": "slab_affine"}
+         "c2a": 65536 * 65536, "c3a": 1024 * 8192 * 8192, "c5a": (1 << 20) * (1 << 20)}
+# c2a / c3a / c5a: the same pairs with the affine constants (2, -3, 5, 2) (bench.py AFFINE_PARAMS)
+WORKLOAD = {"c2": "pair", "c3": "batch", "c5": "slab", "c5p8": "slab_part", "c2a": "pair_affine", "c3a": "batch_affine",
+            "c5a": "slab_affine"}
 
 
 def cells(cfg):
@@ -129,8 +130,11 @@ def main():
     if sys.argv[1] == "--mix-only":
         return mix_only()
     src, rnd = sys.argv[1], sys.argv[2]
+    only = sys.argv[3].split(",") if len(sys.argv) > 3 else None   # e.g. c3a,c5 (default: every pass present)
     prof = os.path.join(ROOT, "profiles")
-    for cfg in ("c2", "c3", "c5", "c5p8", "c2a", "c5a"):
+    for cfg in ("c2", "c3", "c5", "c5p8", "c2a", "c3a", "c5a"):
+        if only is not None and cfg not in only:
+            continue
         stats = os.path.join(src, "kt_" + cfg, cfg + "_kernel_stats.csv")
         if not os.path.exists(stats):
             print("skip", cfg)

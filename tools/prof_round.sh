@@ -16,6 +16,7 @@ for w in $which; do
     c5) args="--workload slab --steps 3 --warmup 1 --cpu-seconds 10"; pargs="--workload slab --steps 2 --warmup 1";;
     c5p8) args="--workload slab --slab-of 8 --steps 3 --warmup 1 --no-cpu-baseline"; pargs="--workload slab --slab-of 8 --steps 2 --warmup 1";;
     c2a) args="--workload pair --params 2,-3,5,2 --steps 10 --warmup 2 --no-cpu-baseline"; pargs="--workload pair --params 2,-3,5,2 --steps 5 --warmup 1";;
+    c3a) args="--workload batch --params 2,-3,5,2 --steps 5 --warmup 1 --no-cpu-baseline"; pargs="--workload batch --params 2,-3,5,2 --steps 3 --warmup 1";;
     c5a) args="--workload slab --params 2,-3,5,2 --steps 3 --warmup 1 --no-cpu-baseline"; pargs="--workload slab --params 2,-3,5,2 --steps 2 --warmup 1";;
   esac
   timeout -k 10 240 python bench.py $args > gpurun_out/prof/bench_$w.json 2> gpurun_out/prof/bench_$w.err
