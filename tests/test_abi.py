@@ -134,7 +134,8 @@ def test_slab_edges_are_system_scope():
     memory model's relaxed system-scope atomic on gfx950); in-GPU edges device
     scope (sc1 only).  Checked on the built code object's disassembly (the
     flow2 kernel template <C, STREAM, RING, SLAB, LIN>, sw_flow2.hip, and flow3's
-    slab kernels sw_flow3rs_kernel / sw_flow3ras_kernel / sw_flow3r3s_kernel, sw_flow3.hip)."""
+    slab kernels sw_flow3rs_kernel / sw_flow3ras_kernel / sw_flow3r3s_kernel / sw_flow3ra3s_kernel,
+    sw_flow3.hip, each named)."""
     import re
     import tempfile
     sys.path.insert(0, os.path.join(ROOT, "tools"))
@@ -173,22 +174,28 @@ def test_slab_edges_are_system_scope():
             assert not sys_ops, (name, sys_ops[:3])
             assert all(" sc1" in x for x in g_stores), name
     assert seen[0] >= 6 and seen[1] >= 3 and pwg >= 2, (seen, pwg)
-    # flow3 (sw_flow3.hip): the slab instantiations of the ring kernel (linear-gap 8-B and affine
-    # 16-B granules) load and store their peer edges system scope; every other flow3 kernel
-    # (staged, ring, affine) keeps its granules device scope
-    f3 = {0: 0, 1: 0}
+    # flow3 (sw_flow3.hip): the slab kernels (linear-gap 8-B and affine 16-B granules, two and three
+    # columns per lane) load and store their peer edges system scope; every other flow3 kernel
+    # (staged, pool loops, ring, affine) keeps its granules device scope.  Named one by one, so a
+    # new kernel (or a renamed one) fails here until it is classified.
+    slab_kernels = {"sw_flow3rs_kernel", "sw_flow3ras_kernel", "sw_flow3r3s_kernel", "sw_flow3ra3s_kernel"}
+    other_kernels = {"sw_flow3_kernel", "sw_flow3a_kernel", "sw_flow3p_kernel", "sw_flow3r_kernel",
+                     "sw_flow3ra_kernel", "sw_flow3r3_kernel", "sw_flow3ra3_kernel"}
+    found = {}
     for name, body in funcs.items():
-        m = re.search(r"sw_flow3(r|ra|rs|ras|a|r3|r3s|p)?_kernel", name)
+        m = re.search(r"\d(sw_flow3[a-z0-9]*_kernel)", name)
         if not m:
             continue
-        slab = m.group(1) in ("rs", "ras", "r3s")
+        base = m.group(1)
+        assert base in slab_kernels | other_kernels, ("unclassified flow3 kernel", name)
         g_ops = [x for x in body if x.startswith(("buffer_load_dwordx2", "buffer_load_dwordx4",
                                                     "buffer_store_dwordx2", "buffer_store_dwordx4"))]
+        assert g_ops, name
         sys_ops = [x for x in g_ops if "sc0 sc1" in x]
-        if slab:
+        if base in slab_kernels:
             assert any(x.startswith("buffer_load") for x in sys_ops), name
             assert any(x.startswith("buffer_store") for x in sys_ops), name
         else:
             assert not sys_ops, (name, sys_ops[:3])
-        f3[slab] += 1
-    assert f3[1] == 3 and f3[0] >= 11, f3
+        found[base] = found.get(base, 0) + 1
+    assert set(found) == slab_kernels | other_kernels, sorted(set(found) ^ (slab_kernels | other_kernels))
