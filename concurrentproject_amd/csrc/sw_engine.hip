@@ -65,7 +65,8 @@ Params g_params;
 std::atomic<long long> g_opt_W{0}, g_opt_C{0}, g_opt_bytes{0}, g_opt_timeout{30}, g_opt_blocks{0}, g_opt_orient{0},
     g_opt_mode{-1}, g_opt_trace{0}, g_opt_duo_f16{1}, g_opt_f2stream{0}, g_opt_ring{-1}, g_opt_ring_rows{4096}, g_opt_f2_wgs{0}, g_opt_f2w{0}, g_opt_f2pwg{-1},
     g_opt_linear{-1}, g_opt_f3{1}, g_opt_slab_plain{0}, g_opt_duo_lds{1}, g_opt_duo_tab{1}, g_opt_duo_roles{1}, g_opt_f3hl{1},
-    g_opt_f3rhl{0}, g_opt_f3a{1}, g_opt_f3slab{1}, g_opt_duo_prio{-1}, g_opt_f3pool{0};
+    g_opt_f3rhl{0}, g_opt_f3a{1}, g_opt_f3slab{1}, g_opt_duo_prio{-1}, g_opt_f3pool{0},
+    g_opt_stall_item{-1};
 
 // Longest sequence the engine takes: granule buffers of m rows keep m * 16 in the
 // 32-bit record count of a buffer resource (sw_device.h linear_edge).
@@ -474,8 +475,9 @@ int finalize_mode(Job& job, const Params& prm, int cus) {
             // three columns per lane (flow3 ring mode, linear-gap step, C = 64; option f2w = 0 or 3): a
             // third fewer strips at 12.5 VALU per 192 cells instead of 9 per 128. C5 165.0 -> 159.5 ms;
             // slab 0 of 8 38.6 -> 33.1 ms (its 1041 two-column strips need 261 groups for 256 CUs, and
-            // the 5 CUs running two pace the chain; 694 three-column strips fit 174 groups)
-            if (job.ring && job.f2w2 && (lin ? g_opt_f3.load() != 0 && g_opt_f3rhl.load() == 0 : g_opt_f3a.load() != 0) &&
+            // the 5 CUs running two pace the chain; 694 three-column strips fit 174 groups).  A slab
+            // with f3slab = 0 stays on flow2's slab kernel, which has no three-column form.
+            if (job.ring && job.f2w2 && (!job.slab || g_opt_f3slab.load() != 0) && (lin ? g_opt_f3.load() != 0 && g_opt_f3rhl.load() == 0 : g_opt_f3a.load() != 0) &&
                 (g_opt_f2w.load() == 3 || g_opt_f2w.load() == 0) && (g_opt_C.load() == 0 || g_opt_C.load() == 64)) {
                 plan_flow2(job, true, false, true);
                 job.ring = true;
@@ -901,13 +903,16 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
     if (duo_wrap > 0) {
         kp.wrap_rows = duo_wrap;
         if (g_opt_duo_roles.load() != 0) kp.ring_cons = c->cons.p;   // per-CU role words (zeroed above)
-        // auto (-1): turn-taking in 1.3 ms slices for one-pass batches (LDS table: one duo per workgroup,
-        // the CU's two workgroups would otherwise end ~3 ms apart, C3 6.48 -> 6.30 ms); off for longer
-        // batches (C4 51.3 -> 51.6 ms with it), profiles/r05_duo_prio.md
+        // auto (-1): turn-taking in 1.3 ms slices whenever the LDS row-code table is used.  That is the
+        // one-pass batches (one duo per workgroup: the CU's two workgroups would otherwise end ~3 ms
+        // apart, C3 6.48 -> 6.30 ms) and, since the table also serves multi-pass batches of rows >= 8192,
+        // those too (8192 pairs of 8192: 51.8 -> 50.5 ms with table + turns); the table-less kernel runs
+        // without turns (profiles/r05_duo_prio.md)
         const int dp = (int)g_opt_duo_prio.load();
         kp.duo_prio = dp >= 0 ? dp : cfg.duo_tab > 0 ? 17 : 0;
     }
     kp.timeout_ticks = g_opt_timeout.load() * 100000000LL;   // s_memrealtime: 100 MHz
+    kp.stall_item = (int)g_opt_stall_item.load();
     kp.trace = reinterpret_cast<unsigned long long*>(g_opt_trace.load());
     if (job.ring) {
         kp.ring_rows = (int)ring_rows;
@@ -1724,6 +1729,9 @@ int sw_set_option(const char* key, long long v) {
     } else if (k == "timeout") {
         if (v < 1 || v > 3600) return -1;
         g_opt_timeout = v;
+    } else if (k == "stall_item") {   // tests only: flow2's compute waves skip this item (-1 = none)
+        if (v < -1) return -1;
+        g_opt_stall_item = v;
     } else if (k == "blocks") {
         if (v < 0) return -1;
         g_opt_blocks = v;
@@ -1806,6 +1814,7 @@ long long sw_get_option(const char* key) {
     if (k == "C") return g_opt_C;
     if (k == "bytes") return g_opt_bytes;
     if (k == "timeout") return g_opt_timeout;
+    if (k == "stall_item") return g_opt_stall_item;
     if (k == "blocks") return g_opt_blocks;
     if (k == "orient") return g_opt_orient;
     if (k == "trace") return g_opt_trace;

@@ -323,16 +323,21 @@ __global__ void __launch_bounds__(f2_threads<STREAM>()) sw_flow2_kernel(KParams 
                     if (SW_F2_LDIDLE > 0 && sent == sent0) __builtin_amdgcn_s_sleep(SW_F2_LDIDLE);
                     // the next window's slots: rows < base + 64 - R must be consumed by wave 0
                     const int floor_rows = min(base, m) + 64 - R;
+                    // the expiry is recorded where it is seen: a second spin_expired call after
+                    // the loop would count one more poll and miss it (n no longer 0 mod 64)
                     while (cseen < floor_rows) {
                         cseen = __builtin_amdgcn_readfirstlane(lds_load(&cons[0]));
                         if (cseen >= floor_rows) break;
                         __builtin_amdgcn_s_sleep(SW_SPIN_SLEEP);
-                        if (spin_expired(spin_n, t0, kp.timeout_ticks)) break;
+                        if (spin_expired(spin_n, t0, kp.timeout_ticks)) {
+                            lfail = true;
+                            break;
+                        }
                     }
-                    if (spin_expired(spin_n, t0, kp.timeout_ticks)) {
-                        lfail = true;
-                        break;
-                    }
+                    // the granule polls above are bounded the same way: the window's rows never
+                    // arriving (a producer that failed) ends the loader as well
+                    if (!lfail && sent == sent0 && spin_expired(spin_n, t0, kp.timeout_ticks)) lfail = true;
+                    if (lfail) break;
                 }
                 if (lfail && lane == 0) {
                     atomicOr(&kp.ctrl->error, ERR_TIMEOUT);
@@ -341,6 +346,7 @@ __global__ void __launch_bounds__(f2_threads<STREAM>()) sw_flow2_kernel(KParams 
             }
             continue;
         }
+        if (item == kp.stall_item) continue;   // tests: this item's edges are never published
         // PWG: this workgroup runs every strip of the pair, wave w the strips w, w + 4, ...
         // (one per round); wave 3 hands off to wave 0 of the next round through LDS too.
         // Positions on every link: row r of round k at k * span + 128 + r (span = the

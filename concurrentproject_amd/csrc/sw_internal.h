@@ -99,6 +99,8 @@ struct KParams {
                                   // duo LDS kernel: DUO_CU_WORDS zeroed role words (or null)
     int duo_prio;                 // duo LDS kernel with roles: 0 = off, k in 6..20 = the CU's two workgroups
                                   // take turns at issue priority every 2^k ticks of s_memrealtime (s_setprio)
+    int stall_item;               // tests only (option stall_item): flow2's compute waves skip this item, so its
+                                  // edges are never published and its consumers' bounded waits must expire; -1 = none
     // (the duo kernel with LDS hand-offs takes its wrap-buffer slots from wrap_rows)
 };
 

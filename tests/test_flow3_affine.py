@@ -159,11 +159,14 @@ def _ring_reset(engine):
     engine.set_option("ring", -1)
     engine.set_option("ring_rows", 4096)
     engine.set_option("blocks", 0)
+    engine.set_option("f2w", 0)
 
 
-def test_flow3ra_ring_parity(engine, oracle_mod, _ring_reset):
+@pytest.mark.parametrize("f2w", [2, 3])
+def test_flow3ra_ring_parity(engine, oracle_mod, _ring_reset, f2w):
     """Ring mode forced on grids of 1, 2, 3 and 7 blocks with 512-row rings (many rounds, the
-    wrap ring every round), rows around the 64-row chunk pairs, the affine constant sets."""
+    wrap ring every round), rows around the 64-row chunk pairs, the affine constant sets; two
+    columns per lane (f2w = 2: sw_flow3ra_kernel) and three (f2w = 3: sw_flow3ra3_kernel)."""
     rng = np.random.default_rng(53)
     pairs = _pairs(rng, [(253, 700), (1009, 513), (2017, 3001), (4096, 2600), (5000, 1200), (9000, 2000),
                          (3025, 127), (2521, 129), (600, 64), (130, 3000)])
@@ -175,16 +178,23 @@ def test_flow3ra_ring_parity(engine, oracle_mod, _ring_reset):
         engine.set_option("linear", 0 if prm[2] == prm[3] else -1)
         for blocks, rows in ((0, 4096), (1, 512), (2, 512), (3, 1024), (7, 512)):
             engine.set_option("ring", 1)
+            engine.set_option("f2w", f2w)
             engine.set_option("blocks", blocks)
             engine.set_option("ring_rows", rows)
             got = []
             for a, b in pairs:
                 got.append(engine.score(a, b, p))
                 st = engine.last_stats()
-                groups = (((len(a) - 2 + 125) // 126 if len(a) > 128 else 1) + 3) // 4
+                if f2w == 3 and st["variant"] & 8192:
+                    strips = 1 if len(a) <= 192 else (len(a) - 3 + 188) // 189
+                else:
+                    strips = (len(a) - 2 + 125) // 126 if len(a) > 128 else 1
+                groups = (strips + 3) // 4
                 if groups > 1:
                     assert st["variant"] & 1024 and st["variant"] & 4 and st["variant"] & 16 and st["C"] == 64, st
                     assert not st["variant"] & (8 | 64), st
+                    # the kernel the option names: sw_flow3ra_kernel (f2w = 2) or sw_flow3ra3_kernel (3)
+                    assert bool(st["variant"] & 8192) == (f2w == 3), st
             assert got == exp, (prm, blocks, rows)
     engine.set_option("linear", -1)
 
@@ -210,6 +220,58 @@ def test_flow3ra_matches_flow2(engine, _ring_reset):
         assert bool(st["variant"] & 1024) == bool(f3a) and st["variant"] & 4, st
         out.append(score.item())
     assert out[0] == out[1] > 0
+
+
+@pytest.mark.parametrize("f2w", [2, 3])
+def test_flow3ra_ring_c2_similar(engine, oracle_mod, golden, _ring_reset, f2w):
+    """The E/F-heavy C2-size pair (C2_affine_similar, 91137: long gaps through every strip, group
+    and ring hand-off) in ring mode on the two- and three-column affine ring kernels, on grids of
+    1-3 workgroups with 512-row rings (the wrap ring every round)."""
+    g = golden("configs.json")["C2_affine_similar"]
+    a, b = oracle_mod.similar_pair(7, g["N"])
+    engine.set_params(engine.Params(*g["params"]))
+    engine.set_option("ring", 1)
+    engine.set_option("f2w", f2w)
+    engine.set_option("ring_rows", 512)
+    for blocks in (1, 2, 3):
+        engine.set_option("blocks", blocks)
+        assert _device_score(engine, a, b) == g["score"], (f2w, blocks)
+        st = engine.last_stats()
+        assert st["variant"] & 1024 and st["variant"] & 4 and bool(st["variant"] & 8192) == (f2w == 3), st
+
+
+def test_flow3ra_c2_similar_slabs(engine, oracle_mod, golden):
+    """The same pair cut into 2 and 4 column slabs (the affine slab kernels, peer edges through
+    slab buffers, threads on one GPU): the max over the slabs is the golden."""
+    from test_slab import _run_threads
+    g = golden("configs.json")["C2_affine_similar"]
+    a, b = oracle_mod.similar_pair(7, g["N"])
+    engine.set_params(engine.Params(*g["params"]))
+    engine.set_option("blocks", 32)          # every slab's grid co-resides on the one GPU
+    try:
+        for nslabs in (2, 4):
+            got, bounds, stats = _run_threads(engine, a, b, nslabs, engine.SW_FLAG_DNA)
+            assert max(got) == g["score"], (nslabs, got, bounds)
+            for st in stats:
+                assert st["variant"] & 1024 and st["variant"] & 2048, st
+    finally:
+        engine.set_option("blocks", 0)
+
+
+def test_flow3ra_config_c5_affine_similar(engine, golden, oracle_mod):
+    """An E/F-heavy pair at C5 size (oracle.similar_pair(20, 2^20), alignments of ~1.5M with
+    indels of up to 4096 bases) at (2, -3, 5, 2) on the default plan (flow3 W3 ring affine),
+    against C5_affine_similar (the oracle's pthread wavefront and the reference's LazySmith)."""
+    cfg = golden("configs.json")
+    if "C5_affine_similar" not in cfg:
+        pytest.skip("C5_affine_similar not pinned yet (tests/golden/gen_pin.py --c5similar)")
+    g = cfg["C5_affine_similar"]
+    a, b = oracle_mod.similar_pair(20, g["N"])
+    engine.set_params(engine.Params(*g["params"]))
+    assert _device_score(engine, a, b) == g["score"]
+    st = engine.last_stats()
+    assert st["variant"] & 1024 and st["variant"] & 4 and st["variant"] & 8192, st
+    assert st["boundary_bytes"] < 1 << 30, st
 
 
 def test_flow3ra_config_c5_affine(engine, golden):

@@ -277,6 +277,39 @@ def test_flow2_loader_wave(engine, oracle_mod):
         engine.set_option("orient", 0)
 
 
+def test_flow2_loader_wave_timeout(engine, oracle_mod):
+    """A producer group that never publishes (test option stall_item: flow2's compute waves skip
+    item 0) makes the next group's loader wave and wave 0 wait in vain: their bounded spins expire,
+    the launch reports ERR_TIMEOUT (SwError) within seconds instead of hanging, and the engine
+    scores the next launch correctly.  Staged flow2 kernel, one column per lane, affine step."""
+    import time
+    rng = np.random.default_rng(77)
+    a, b = _rand_dna(rng, 2000), _rand_dna(rng, 500)       # 32 strips: 8 groups, loader in groups 1..7
+    prm = engine.Params(2, -3, 5, 2)
+    engine.set_option("orient", 1)
+    engine.set_option("mode", 5)
+    engine.set_option("f3a", 0)                             # flow2's affine step (staged, loader wave)
+    engine.set_option("timeout", 1)
+    try:
+        engine.set_option("stall_item", 0)
+        assert engine.get_option("stall_item") == 0
+        t0 = time.time()
+        with pytest.raises(engine.SwError):
+            engine.score(a, b, prm)
+        assert time.time() - t0 < 60
+        st = engine.last_stats()
+        assert st["mode"] == 5 and not st["variant"] & (2 | 64 | 1024), st   # flow2 staged, no flow3
+        engine.set_option("stall_item", -1)
+        op = oracle_mod.Params(2, -3, 5, 2)
+        assert engine.score(a, b, prm) == oracle_mod.score_linear(a, b, op)
+    finally:
+        engine.set_option("stall_item", -1)
+        engine.set_option("timeout", 5)
+        engine.set_option("f3a", 1)
+        engine.set_option("mode", -1)
+        engine.set_option("orient", 0)
+
+
 def test_flow2_streamed_rows(engine, oracle_mod):
     """flow2 with the row codes streamed through per-wave LDS rings (rows too long
     to stage, the C5 path): forced on the ragged flow2 shapes and chosen

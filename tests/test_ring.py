@@ -38,7 +38,17 @@ def _pairs(rng):
     return out
 
 
-def test_ring_mode_matches_oracle(engine, oracle_mod):
+def _strips(n, variant):
+    """Strips of the single-pair kernel that ran: 189 columns (W3, variant 8192), 126 (W2, 16) or 63."""
+    if variant & 8192:
+        return 1 if n <= 192 else (n - 3 + 188) // 189
+    if variant & 16:
+        return (n - 2 + 125) // 126 if n > 128 else 1
+    return (n - 1 + 62) // 63
+
+
+@pytest.mark.parametrize("f2w", [2, 3])
+def test_ring_mode_matches_oracle(engine, oracle_mod, f2w):
     """Forced ring mode on grids of 1, 2, 3 and 7 blocks (many rounds, the wrap
     ring used every round) and rings of 512 rows (rows wrap them several times),
     default and G_INIT != G_EXT constants.  Ring mode always runs the streamed-code
@@ -50,6 +60,7 @@ def test_ring_mode_matches_oracle(engine, oracle_mod):
     engine.set_option("orient", 1)
     engine.set_option("mode", 5)
     engine.set_option("ring", 1)
+    engine.set_option("f2w", f2w)   # two columns per lane (sw_flow2 / sw_flow3ra) or three (flow3 W3)
     for prm in (engine.Params(), engine.Params(2, -3, 5, 2), engine.Params(3, -2, 4, 4)):
         op = oracle_mod.Params(prm.match, prm.mismatch, prm.gap_init, prm.gap_ext)
         exp = [oracle_mod.score_linear(a, b, op) for a, b in pairs]
@@ -60,10 +71,11 @@ def test_ring_mode_matches_oracle(engine, oracle_mod):
             for a, b in pairs:
                 got.append(engine.score(a, b, prm))
                 st = engine.last_stats()
-                n = len(a)
-                strips = ((n - 2 + 125) // 126 if n > 128 else 1) if st["variant"] & 16 else (n - 1 + 62) // 63
-                groups = (strips + 3) // 4
+                groups = (_strips(len(a), st["variant"]) + 3) // 4
                 assert st["mode"] == 5 and bool(st["variant"] & 4) == (groups > 1), st
+                # f2w = 2 keeps the two-column ring kernels; f2w = 3 takes three columns in ring mode
+                assert not (f2w == 2 and st["variant"] & 8192), st
+                assert not (f2w == 3 and st["variant"] & 4) or st["variant"] & 8192, st
                 # two columns per lane when the linear-gap step runs (G_INIT == G_EXT), and in ring
                 # mode for the affine step too (flow3's sw_flow3ra_kernel, variant bit 1024)
                 ring_aff = bool(st["variant"] & 4 and st["variant"] & 1024)

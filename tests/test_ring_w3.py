@@ -182,3 +182,31 @@ def test_w3_affine_slabs(engine, oracle_mod, nslabs):
         assert all(x % 189 == 0 for x in bounds[1:-1]), bounds
         for s in stats:
             assert s["variant"] & 8192 and s["variant"] & 1024 and s["variant"] & 2048, s
+
+
+def test_f3slab_off_keeps_flow2_slab_kernel(engine, oracle_mod):
+    """Option f3slab = 0 keeps a ring-mode column slab on flow2's slab kernel (no three-column form):
+    slab bounds on its strip stride (not 189), the slabs score the pair, and the same cut with
+    f3slab = 1 runs flow3's three-column slab kernel to the same maximum."""
+    rng = np.random.default_rng(81)
+    a = _rand_dna(rng, 2 * 2000 + 77)
+    b = _similar(rng, a, 1500)
+    exp = oracle_mod.score_linear(a, b, oracle_mod.Params(1, -1, 1, 1))
+    engine.set_option("ring", 1)
+    engine.set_option("ring_rows", 512)
+    engine.set_option("blocks", 3)
+    try:
+        engine.set_option("f3slab", 0)
+        q0 = engine.slab_bounds(len(a), len(b), 2, engine.SW_FLAG_DNA)
+        got, bounds, stats = _run_threads(engine, a, b, 2, engine.SW_FLAG_DNA)
+        assert bounds == q0 and max(got) == exp, (got, exp, bounds)
+        for st in stats:
+            assert st["mode"] == 5 and st["variant"] & 4 and not st["variant"] & (2048 | 8192), st
+        assert bounds[1] % 63 == 0, bounds   # flow2's strip stride (63 or 126 columns)
+        engine.set_option("f3slab", 1)
+        got1, bounds1, stats1 = _run_threads(engine, a, b, 2, engine.SW_FLAG_DNA)
+        assert max(got1) == exp and bounds1[1] % 189 == 0, (got1, bounds1)
+        for st in stats1:
+            assert st["variant"] & 2048 and st["variant"] & 8192, st
+    finally:
+        engine.set_option("f3slab", 1)
