@@ -204,6 +204,7 @@ struct Job {
     bool ring = false;           // MODE_FLOW2, one pair: group edges through per-block rings (O(m) state)
     bool f2w2 = false;           // MODE_FLOW2: two columns per lane (strips of 126 new columns, LIN step)
     bool f2w3 = false;           // ... three (strips of 189; with f2w2: flow3 ring mode only, sw_flow3r3_kernel)
+    int w45_s4 = -1;             // with f2w3: four / five columns per lane instead (sw_flow3r45_kernel, plan_w45)
     bool pwg = false;            // MODE_FLOW2 batch: a pair per workgroup (sw_flow2.hip PWG)
 };
 
@@ -368,6 +369,35 @@ bool flow2_w2_wanted(const Job& job, const Params& p) {
     return lin && o != 1;
 }
 
+// Four and five columns per lane (flow3 ring mode, linear-gap step, one pair): when the three-column
+// strips need more groups than `slots` resident blocks (C5: 5549 strips in 1388 groups for 1024), the
+// later groups run in a second round after the first ones end, at a fraction of the chip (C5 154 ms
+// against a 115 ms issue bound; tools/sim_ring.py models it at 151).  Strips of 252 new columns, then
+// g5 groups of 315, fit `slots` groups: 1008 (slots - g5) + 1260 g5 >= n.  A group's four strips share a
+// width, so the split index s4 is a multiple of 4.  Modelled 142 ms for C5 (every strip resident), but
+// measured 167 ms against W3's 154 (r06, profiles/r06_c5_w45.md): strip 0, which runs at the lone-wave
+// pace, takes 42.5 ms at four columns against 29.7 at three, and the later strips end at the same
+// 0.119 us per column in both.  So it is an option (f2w = 4), not the automatic plan.
+// Returns false (plan unchanged) when n needs more than five columns per lane.
+bool plan_w45(Job& job, int slots) {
+    PairDesc& d = job.pairs[0];
+    const long long n = d.n;
+    const long long g5 = std::max(0LL, (n - 1008LL * slots + 251) / 252);
+    if (g5 > slots || n < 4 * 256) return false;
+    int s4 = 4 * (int)(slots - g5), s5 = 0;
+    if (252LL * (s4 - 1) + 256 < n) {
+        // W5 strips after s4 W4 strips: the last one's columns reach n - 1
+        s5 = (int)std::max(1LL, (n - 320 - 252LL * s4 + 314) / 315 + 1);
+    } else {
+        // four columns cover it: the fewest W4 strips (no W5 strip, so s4 may be any count)
+        s4 = (int)std::max(1LL, (n - 256 + 251) / 252 + 1);
+    }
+    d.strips = s4 + s5;
+    job.w45_s4 = s5 > 0 ? s4 : d.strips;
+    job.item_base[1] = job.item_base[0] + (d.strips + 3) / 4;
+    return true;
+}
+
 // Re-plan a grouped job for MODE_FLOW2: strips of 64 columns overlapping by one
 // (w2: 128 columns overlapping by two).  pwg: one item per pair, whose workgroup runs all
 // of its strips with LDS hand-offs only (no granule edges).
@@ -478,9 +508,16 @@ int finalize_mode(Job& job, const Params& prm, int cus) {
             // the 5 CUs running two pace the chain; 694 three-column strips fit 174 groups).  A slab
             // with f3slab = 0 stays on flow2's slab kernel, which has no three-column form.
             if (job.ring && job.f2w2 && (!job.slab || g_opt_f3slab.load() != 0) && (lin ? g_opt_f3.load() != 0 && g_opt_f3rhl.load() == 0 : g_opt_f3a.load() != 0) &&
-                (g_opt_f2w.load() == 3 || g_opt_f2w.load() == 0) && (g_opt_C.load() == 0 || g_opt_C.load() == 64)) {
+                (g_opt_f2w.load() == 3 || g_opt_f2w.load() == 0 || g_opt_f2w.load() == 4) &&
+                (g_opt_C.load() == 0 || g_opt_C.load() == 64)) {
                 plan_flow2(job, true, false, true);
                 job.ring = true;
+                // ... or four and five with option f2w = 4 (every group resident in one round; measured
+                // slower on C5, 167 against 154 ms: plan_w45).  Its grid is F2_WGS_MAX blocks per CU, or
+                // option blocks (tests cut small pairs into both widths with it)
+                const long long w = g_opt_f2w.load();
+                const int slots = g_opt_blocks.load() > 0 ? (int)g_opt_blocks.load() : cus * F2_WGS_MAX;
+                if (lin && !job.slab && job.pairs.size() == 1 && w == 4) plan_w45(job, slots);
             }
             job.f2_stream = job.ring || !flow2_staged(job, max_m);   // ring mode runs with streamed codes
             // ring mode (one pair of many groups per CU, C5): throughput-bound, so 64-row chunks
@@ -748,7 +785,8 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
         probe.f2_w2 = job.f2w2;
         probe.f3_hl = use_f3 && job.C == 64 && g_opt_f3rhl.load() != 0;
         probe.f3ra = use_f3ra;
-        probe.f3_w3 = (use_f3 || use_f3ra) && job.f2w3;
+        probe.f3_w3 = (use_f3 || use_f3ra) && job.f2w3 && job.w45_s4 < 0;
+        probe.f3_w45 = use_f3 && job.w45_s4 >= 0;
         probe.f3_slab = (use_f3 || use_f3ra) && edge != nullptr;
         if (probe.f3_slab) probe.f3_hl = false;
         int fit = 0;
@@ -831,7 +869,12 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
     // the pool loops (no I/O rotation, tools/gen_flow3.py gen_pool) for staged launches with
     // half-chunk links at C = 32, both steps, when option f3pool = 1 (default 0: measured slower)
     cfg.f3p = g_opt_f3pool.load() != 0 && cfg.f3_hl && job.C == 32 && !job.ring && (use_f3 || use_f3a);
-    cfg.f3_w3 = job.f2w3;
+    cfg.f3_w3 = job.f2w3 && job.w45_s4 < 0;
+    cfg.f3_w45 = job.w45_s4 >= 0;
+    if (cfg.f3_w45 && !(use_f3 && job.ring && edge == nullptr)) {
+        set_err("four / five columns per lane run on flow3's linear-gap ring kernel only (one pair, not a slab)");
+        return -1;
+    }
     if (job.f2w3 && !((use_f3 || use_f3ra) && job.ring && job.C == 64 && !cfg.f3_hl)) {
         set_err("three columns per lane run on flow3's ring kernel only (linear-gap step, C = 64, whole-chunk links)");
         return -1;
@@ -913,6 +956,7 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
     }
     kp.timeout_ticks = g_opt_timeout.load() * 100000000LL;   // s_memrealtime: 100 MHz
     kp.stall_item = (int)g_opt_stall_item.load();
+    kp.w45_s4 = cfg.f3_w45 ? job.w45_s4 : -1;
     kp.trace = reinterpret_cast<unsigned long long*>(g_opt_trace.load());
     if (job.ring) {
         kp.ring_rows = (int)ring_rows;
@@ -942,7 +986,8 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
     t_stats.variant = (cfg.duo_f16 ? 1 : 0) | (cfg.f2_stream ? 2 : 0) | (job.ring ? 4 : 0) | (cfg.f2_lin ? 8 : 0) |
                       (cfg.f2_w2 ? 16 : 0) | (cfg.f2_pwg ? 32 : 0) | (cfg.f3 ? 64 : 0) | (cfg.duo_wrap > 0 ? 128 : 0) |
                       (cfg.duo_tab > 0 ? 256 : 0) | (cfg.f3_hl ? 512 : 0) | (cfg.f3a || cfg.f3ra ? 1024 : 0) |
-                      (cfg.f3_slab ? 2048 : 0) | (cfg.f3p ? 4096 : 0) | (cfg.f3_w3 ? 8192 : 0);
+                      (cfg.f3_slab ? 2048 : 0) | (cfg.f3p ? 4096 : 0) | (cfg.f3_w3 ? 8192 : 0) |
+                      (cfg.f3_w45 ? 16384 : 0);
     t_stats.boundary_bytes = (long long)(job.bnd_granules * sizeof(Granule));
     c->last = s;
     return 0;
@@ -1751,8 +1796,9 @@ int sw_set_option(const char* key, long long v) {
         if (v < 0 || v > F2_WGS_MAX) return -1;
         g_opt_f2_wgs = v;
     } else if (k == "f2w") {   // flow2 columns per lane: 0 auto, 1, 2 (2: the linear-gap step only),
-        // 3 (flow3 ring mode with the linear-gap step: single long pairs and column slabs; auto there)
-        if (v < 0 || v > 3) return -1;
+        // 3 (flow3 ring mode with the linear-gap step: single long pairs and column slabs; auto there),
+        // 4 (four / five columns per lane in that ring mode, one pair, every group in one round)
+        if (v < 0 || v > 4) return -1;
         g_opt_f2w = v;
     } else if (k == "f2pwg") {   // int32 DNA batches on flow2, a pair per workgroup: -1 auto, 0 off, 1 forced
         if (v < -1 || v > 1) return -1;

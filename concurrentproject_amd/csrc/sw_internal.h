@@ -99,6 +99,8 @@ struct KParams {
                                   // duo LDS kernel: DUO_CU_WORDS zeroed role words (or null)
     int duo_prio;                 // duo LDS kernel with roles: 0 = off, k in 6..20 = the CU's two workgroups
                                   // take turns at issue priority every 2^k ticks of s_memrealtime (s_setprio)
+    int w45_s4;                   // flow3 ring at four / five columns per lane (sw_flow3r45_kernel): strips below
+                                  // this index have 252 new columns, the rest 315 (a multiple of 4); -1 otherwise
     int stall_item;               // tests only (option stall_item): flow2's compute waves skip this item, so its
                                   // edges are never published and its consumers' bounded waits must expire; -1 = none
     // (the duo kernel with LDS hand-offs takes its wrap-buffer slots from wrap_rows)
@@ -142,6 +144,7 @@ struct LaunchCfg {
     bool f3a = false;       // MODE_FLOW2 staged one-column launch with the affine step on flow3 (sw_flow3a_kernel)
     bool f3p = false;       // flow3 staged on the pool loops (sw_flow3p_kernel: C = 32, f3_hl, no I/O rotation)
     bool f3_w3 = false;     // flow3 ring mode at three columns per lane (sw_flow3r3_kernel / sw_flow3r3s_kernel)
+    bool f3_w45 = false;    // flow3 ring mode at four and five columns per lane (sw_flow3r45_kernel, KParams::w45_s4)
     bool f3ra = false;      // MODE_FLOW2 ring-mode two-column launch with the affine step on flow3 (sw_flow3ra_kernel)
     bool f3_slab = false;   // flow3 ring launch of a column slab (sw_flow3rs_kernel / sw_flow3ras_kernel)
     int duo_wrap = 0;       // MODE_DUO at C = 64: > 0 = strip hand-offs in LDS (sw_duo_lds_kernel), this many

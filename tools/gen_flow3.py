@@ -419,6 +419,47 @@ RING = dict(H="v42", HGO="v43", HB="v44", HGOB="v45", TA="v46", TB="v47", PA="v4
 RING3 = dict(RING, HC="v108", HGOC="v109", TC0="v110", TC1="v111", PC="v112")
 
 
+# four and five columns per lane (ring mode, sw_flow3.hip flow3_ring<..., W45>: C5-sized pairs whose
+# three-column strips outnumber the resident slots): column D's H, max(H_D - G, 0), t, score bytes;
+# column E's H, max(H_E - G, 0), t of even / odd steps, score bytes.  The kernel's fixed registers stay
+# below v122 (128 VGPRs: 4 waves per SIMD).
+RING4 = dict(RING3, TC="v110", HD="v113", HGOD="v114", TD="v115", PD="v116")
+RING5 = dict(RING4, HE="v117", HGOE="v118", TE0="v119", TE1="v120", PE="v121")
+COLS = "ABCDE"
+
+
+def colreg(r, c, what):
+    """Register of column c (0..4) in a ring step map: what in H, HGO, P."""
+    if c == 0:
+        return {"H": r["H"], "HGO": r["HGO"], "P": r["PA"]}[what]
+    return r[what + COLS[c]]
+
+
+def step_w(a, io, l0, b, r, W):
+    """One anti-diagonal step of the W-column linear-gap step (W = 4, 5; 64 W cells): step3 with
+    more columns.  Every column's t first (column c's diagonal is column c-1's H of the last
+    step), then the lane hand-off of the last column, then the column chain left to right
+    (H_c = max3(left, up, t_c), HGO_c = max(H_c - G, 0)); the running max takes the t's in pairs
+    (A,B), (C,D) every step and, at W = 5, column E's t of two steps on odd steps."""
+    assert W in (4, 5)
+    t = ["v46", "v47", "v110", "v115"] + ([r["TE1"] if b % 2 else r["TE0"]] if W == 5 else [])
+    diag = [l0] + [colreg(r, c, "H") for c in range(W - 1)]
+    for c in range(W):
+        a(f"v_add_u32_sdwa {t[c]}, sext({colreg(r, c, 'P')}), {diag[c]} dst_sel:DWORD dst_unused:UNUSED_PAD "
+          f"src0_sel:BYTE_{b} src1_sel:DWORD")
+    a(f"v_mov_b32_dpp {l0}, {io} wave_shl:1 row_mask:0xf bank_mask:0xf")
+    a(f"v_add_u32_dpp {io}, {colreg(r, W - 1, 'H')}, %[ng] wave_shr:1 row_mask:0xf bank_mask:0xf")
+    left = io
+    for c in range(W):
+        a(f"v_max3_i32 {colreg(r, c, 'H')}, {left}, {colreg(r, c, 'HGO')}, {t[c]}")
+        a(f"v_sub_u32_e64 {colreg(r, c, 'HGO')}, {colreg(r, c, 'H')}, %[G] clamp")
+        left = colreg(r, c, "HGO")
+    a(f"v_max3_i32 {r['M']}, {r['M']}, {t[0]}, {t[1]}")
+    a(f"v_max3_i32 {r['M']}, {r['M']}, {t[2]}, {t[3]}")
+    if W == 5 and b % 2:
+        a(f"v_max3_i32 {r['M']}, {r['M']}, {r['TE0']}, {r['TE1']}")
+
+
 def step3(a, io, l0, b, r):
     """One anti-diagonal step of the three-column linear-gap step (12.5 VALU, 192 cells): columns
     A, B, C = 3 lane, + 1, + 2; the left input of A is lane l-1's column C (the DPP-add), of B and
@@ -497,8 +538,10 @@ def gen_role_ring(IN, OUT_, C=64, hl=False, W=2):
     # ---- entry (s_nop 4: descriptor operands may be fresh from v_readfirstlane)
     a("s_nop 4")
     a("s_waitcnt vmcnt(0) lgkmcnt(0)")
-    assert W in (2, 3) and (W == 2 or (C == 64 and not hl))
-    for r in ("v42", "v43", "v44", "v45", "v50") + (("v108", "v109") if W == 3 else ()):
+    assert W in (2, 3, 4, 5) and (W == 2 or (C == 64 and not hl))
+    zero = ("v42", "v43", "v44", "v45", "v50") + (("v108", "v109") if W >= 3 else ()) + \
+        (("v113", "v114") if W >= 4 else ()) + (("v117", "v118") if W == 5 else ())
+    for r in zero:
         a(f"v_mov_b32 {r}, 0")
     a("v_mov_b32 v40, %[ng]")
     a("v_mov_b32 v41, %[ng]")
@@ -660,11 +703,17 @@ def gen_role_ring(IN, OUT_, C=64, hl=False, W=2):
                     a("v_cndmask_b32_e64 v40, v102, v40, %[lhi]")
             a(f"v_perm_b32 v48, %[pA], %[k80], v{cur + u}")
             a(f"v_perm_b32 v49, %[pB], %[k80], v{cur + u}")
-            if W == 3:
+            if W >= 3:
                 a(f"v_perm_b32 v112, %[pC], %[k80], v{cur + u}")
+            if W >= 4:
+                a(f"v_perm_b32 v116, %[pD], %[k80], v{cur + u}")
+            if W == 5:
+                a(f"v_perm_b32 v121, %[pE], %[k80], v{cur + u}")
             for b in range(4):
                 io, l0 = ("v40", "v41") if b % 2 == 0 else ("v41", "v40")
-                if W == 3:
+                if W >= 4:
+                    step_w(a, io, l0, b, RING5 if W == 5 else RING4, W)
+                elif W == 3:
                     step3(a, io, l0, b, RING3)
                 else:
                     step(a, io, l0, b, RING)
@@ -874,6 +923,48 @@ def emit_ring3():
         out.append("}")
         out.append("")
     return "\n".join(out)
+
+OUT_RING45 = os.path.join(ROOT, "concurrentproject_amd", "csrc", "sw_flow3r45_loops.inc")
+
+
+def emit_ring45():
+    """Four and five columns per lane in ring mode (sw_flow3.hip sw_flow3r45_kernel: a C5-sized
+    pair cut into 252-column strips and, at its end, 315-column ones, so that every strip is
+    resident in one round): C = 64, whole-chunk links, the nine ring roles, no slab roles."""
+    out = ["// GENERATED by tools/gen_flow3.py -- do not edit.  The flow3 ring-mode chunk loops at four and",
+           "// five columns per lane (sw_flow3.hip sw_flow3r45_kernel): one inline-asm block per (W, strip role),",
+           "// C = 64, R = %d.  Operands: see F3RLoop in sw_flow3.hip; fixed registers: tools/gen_flow3.py (RING4/5)." % RR,
+           "#pragma once", ""]
+    for W in (4, 5):
+        clob = CLOBBERS_RING3 + ['"v%d"' % r for r in range(113, 117 if W == 4 else 122)]
+        for IN in ROLES_IN_RING:
+            for OUT_ in ROLES_OUT:
+                body = gen_role_ring(IN, OUT_, 64, False, W)
+                out.append("template <> __device__ __forceinline__ F3Res f3r%d_loop<F3_%s, F3_%s>(const F3RLoop& x) {"
+                           % (W, IN.upper(), OUT_.upper()))
+                out.append("    F3Res r;")
+                out.append("    asm volatile(")
+                for line in body:
+                    out.append('        "%s\\n\\t"' % line)
+                out.append('        : [M] "=v"(r.M), [fail] "=s"(r.fail), [slow] "=s"(r.slow)')
+                out.append('        : [pA] "v"(x.pA), [pB] "v"(x.pB), [pC] "v"(x.pC), [pD] "v"(x.pD),' +
+                           (' [pE] "v"(x.pE),' if W == 5 else '') + ' [ng] "v"(x.ng), [G] "s"(x.G), [k80] "s"(x.k80),')
+                out.append('          [m] "s"(x.m), [end] "s"(x.end), [dlo] "s"(x.dlo), [dhi] "s"(x.dhi), [lane] "v"(x.lane),')
+                out.append('          [raw2] "v"(x.raw2), [cro] "v"(x.cro), [c0] "v"(x.c0), [cbase] "v"(x.cbase),')
+                out.append('          [cwr] "v"(x.cwr), [cwm] "v"(x.cwm), [rrs] "s"(x.rrs), [rrow] "v"(x.rrow),')
+                out.append('          [lin] "v"(x.lin), [lout] "v"(x.lout), [pin] "v"(x.pin), [pout] "v"(x.pout),')
+                out.append('          [qme] "v"(x.qme), [qnx] "v"(x.qnx),')
+                out.append('          [girs] "s"(x.girs), [gioff] "v"(x.gioff), [gipos] "v"(x.gipos), [gimask8] "s"(x.gimask8),')
+                out.append('          [ek] "s"(x.ek), [cross] "s"(x.cross), [crv0] "s"(x.crv0), [croff] "v"(x.croff),')
+                out.append('          [gors] "s"(x.gors), [gooff] "v"(x.gooff), [gopos] "v"(x.gopos), [gomask8] "s"(x.gomask8),')
+                out.append('          [gorow] "v"(x.gorow), [lhi] "s"(x.lhi), [bpr] "s"(x.bpr), [bpbase] "s"(x.bpbase),')
+                out.append('          [lmid] "v"(x.lmid), [ekp] "s"(x.ekp)')
+                out.append("        : " + ", ".join(clob) + ");")
+                out.append("    return r;")
+                out.append("}")
+                out.append("")
+    return "\n".join(out)
+
 
 # ============================================================================================
 # The general affine (Gotoh) step, staged organisation (C2 with G_INIT != G_EXT):
@@ -1915,6 +2006,7 @@ def main():
     text = emit(spec, halfpub)
     text_pool = emit_pool()
     text_ring3 = emit_ring3()
+    text_ring45 = emit_ring45()
     text_ring = emit_ring()
     text_aff = emit_aff()
     text_ring_aff = emit_ring_aff()
@@ -1925,12 +2017,15 @@ def main():
         cur_ra = open(OUT_RING_AFF).read() if os.path.exists(OUT_RING_AFF) else ""
         cur_p = open(OUT_POOL).read() if os.path.exists(OUT_POOL) else ""
         cur_r3 = open(OUT_RING3).read() if os.path.exists(OUT_RING3) else ""
+        cur_r45 = open(OUT_RING45).read() if os.path.exists(OUT_RING45) else ""
         sys.exit(0 if cur == text and cur_r == text_ring and cur_a == text_aff and cur_ra == text_ring_aff and
-                 cur_p == text_pool and cur_r3 == text_ring3 else 1)
+                 cur_p == text_pool and cur_r3 == text_ring3 and cur_r45 == text_ring45 else 1)
     with open(OUT_POOL, "w") as f:
         f.write(text_pool)
     with open(OUT_RING3, "w") as f:
         f.write(text_ring3)
+    with open(OUT_RING45, "w") as f:
+        f.write(text_ring45)
     with open(OUT_AFF, "w") as f:
         f.write(text_aff)
     with open(OUT_RING_AFF, "w") as f:

@@ -34,8 +34,9 @@ def step_mix(W, affine=False):
 
 
 def simulate(widths, cus=256, blocks_per_cu=4, lag=100, ring_in=512, ring_x=4096, m=1 << 20, ovh=1.0,
-             dt=2000.0, affine=False, max_ms=600.0):
-    """widths: columns per lane of every strip (in chain order).  Returns (ms, per-round stats)."""
+             dt=2000.0, affine=False, max_ms=600.0, timeline=False):
+    """widths: columns per lane of every strip (in chain order).  Returns (ms, per-round stats);
+    timeline: also each strip's first-step and end times (ns)."""
     S = len(widths)
     G = cus * blocks_per_cu
     groups = (S + 3) // 4
@@ -57,6 +58,7 @@ def simulate(widths, cus=256, blocks_per_cu=4, lag=100, ring_in=512, ring_x=4096
     # of the next round) of m rows: no back-pressure
     ring_lim = np.where((s_idx % 4) == 3, np.where(grp % G == G - 1, m + 64, ring_x), ring_in) + 63
     t = 0.0
+    first = np.full(S, np.nan)
     nsimd = cus * 4
     while np.isnan(done_at).any() and t < max_ms * 1e6:
         active = (start <= t) & np.isnan(done_at)
@@ -90,6 +92,7 @@ def simulate(widths, cus=256, blocks_per_cu=4, lag=100, ring_in=512, ring_x=4096
         p_new = np.maximum(p_new, p)
         fin = (p_new >= steps_total) & np.isnan(done_at)
         done_at[fin] = t + dt
+        first[(p_new > 0) & np.isnan(first)] = t
         p = p_new
         t += dt
         # groups whose block finished its previous group start now
@@ -106,7 +109,10 @@ def simulate(widths, cus=256, blocks_per_cu=4, lag=100, ring_in=512, ring_x=4096
             ready[nxt_g[ok & gdone]] = True
             newly = ready[grp] & np.isinf(start)
             start[newly] = t
-    return t / 1e6, {"strips": S, "groups": groups, "rounds": int(rnd.max()) + 1}
+    st = {"strips": S, "groups": groups, "rounds": int(rnd.max()) + 1}
+    if timeline:
+        return t / 1e6, st, first, done_at
+    return t / 1e6, st
 
 
 def widths_mix(n4, n5):
