@@ -276,8 +276,8 @@ def kernel_label(st):
         ring, w2, f3, hl, aff3 = bool(v & 4), bool(v & 16), bool(v & 64), bool(v & 512), bool(v & 1024)
         if f3 or aff3:
             name = ("flow3 ring" if ring else "flow3") + (" affine" if aff3 else "") + (" W3" if v & 8192 else "") + \
-                (" pool loops" if v & 4096 else "")
-            fn = "sw_flow3p_kernel" if v & 4096 else \
+                (" W4/W5" if v & 16384 else "") + (" pool loops" if v & 4096 else "")
+            fn = "sw_flow3p_kernel" if v & 4096 else "sw_flow3r45_kernel" if v & 16384 else \
                 ("sw_flow3r" if ring else "sw_flow3") + ("a" if aff3 else "") + ("3" if v & 8192 else "") + \
                 ("s" if v & 2048 else "") + "_kernel"
             if v & 2048:
@@ -287,7 +287,7 @@ def kernel_label(st):
             fn = "sw_flow2_kernel"
         if hl:
             name += ", half-chunk links"
-        out["W"] = 3 if v & 8192 else 2 if w2 else 1
+        out["W"] = 4 if v & 16384 else 3 if v & 8192 else 2 if w2 else 1
     elif mode == 3:
         name = "duo" + (" LDS hand-offs" if v & 128 else " granules") + (", row-code table" if v & 256 else "") + \
                (", f16-max3" if v & 1 else "")

@@ -183,14 +183,19 @@ void sw_db_close(sw_db* db);
  *   "mode"     -1 = auto, 0 = independent strip waves, 1 = workgroup per pair,
  *              2 = lock-step strip groups (single long pairs),
  *              3 = packed 16-bit pair duos (DNA batches with scores < 65535),
- *              4 = free-running strip groups, rows staged in LDS (long DNA pairs)
+ *              4 = free-running strip groups, rows staged in LDS (long DNA pairs),
+ *              5 = the flow2 / flow3 wavefront step (DNA, one column per lane or more, chunked
+ *                  LDS / granule hand-offs; the automatic plan for single long pairs, column
+ *                  slabs and batches whose scores need int32)
  *   "duo16"    1 = (default) packed duos take max3 through v_pk_maximum3_f16 when every
  *              value stays below 0x7C00 (MATCH*(min(n,m)+1) <= 31743), 0 = u16 max only
  *   "linear"   -1 = (default) the exact linear-gap step when G_INIT == G_EXT
  *              (flow2 C = 32 or 64, f16 duos), 0 = always the affine step
  *   "f2w"      flow2 columns per lane: 0 = (default) two whenever the linear-gap
  *              step runs (three in flow3 ring mode: C5, column slabs), one otherwise;
- *              1 = always one; 2 = two (linear-gap step only); 3 = three where ring mode runs
+ *              1 = always one; 2 = two (linear-gap step only); 3 = three where ring mode runs;
+ *              4 = four / five in ring mode for one pair, every strip group resident in one round
+ *              (sw_flow3r45_kernel; measured slower than three on C5, so never automatic)
  *   "f3pool"   1 = flow3 staged launches on the loops without the I/O rotation (measured
  *              slower; default 0)
  *   "ring"     -1 = (default) ring edges for a single flow2 pair whose linear edges
@@ -209,6 +214,10 @@ void sw_db_close(sw_db* db);
  *              hand off every half chunk (16 rows); 0 = whole-chunk links at C = 16 (auto C)
  *   "f3rhl"    1 = flow3 ring launches (C = 64) with half-chunk in-workgroup links (32 rows),
  *              0 = (default) whole-chunk links (measured faster on C5)
+ *   "f3a"      1 = (default) the general affine step runs on flow3 (staged: sw_flow3a_kernel, one
+ *              column per lane, C2 with G_INIT != G_EXT; ring: sw_flow3ra(3)_kernel, C5), 0 = flow2
+ *   "f3slab"   1 = (default) column slabs run flow3's ring kernel with slab roles
+ *              (sw_flow3rs / ras / r3s / ra3s_kernel), 0 = flow2's slab kernel
  *   "duo_lds"  1 = (default) duo batches at C = 64 hand strip edges on in LDS when a round's
  *              rows fit (m <= 16384 linear-gap step, 8192 affine), 0 = through HBM granules
  *   "duo_roles" 1 = (default) the two duo LDS workgroups of a CU take complementary strip roles
@@ -223,6 +232,8 @@ void sw_db_close(sw_db* db);
  *   "slab_plain" 1 = an exported slab buffer may fall back to plain device memory (one-GPU
  *              tests only; cross-GPU edges need fine-grained memory), 0 = (default) refuse
  *   "trace"    device address of a 16 x u64 per-strip trace buffer, 0 = off (tools)
+ *   "stall_item" tests only: flow2's compute waves skip this item (its edges are never
+ *              published, so its consumers' bounded waits expire: ERR_TIMEOUT); -1 = (default) none
  * Returns 0, or -1 for an unknown key / bad value. */
 int sw_set_option(const char* key, long long value);
 long long sw_get_option(const char* key);
@@ -241,7 +252,12 @@ typedef struct {
                                bit 6: the flow3 kernel (sw_flow3.hip);
                                bit 7: duo strip hand-offs in LDS (no boundary buffers);
                                bit 8: duo row codes from an LDS table;
-                               bit 9: flow3 half-chunk LDS links (option f3hl) */
+                               bit 9: flow3 half-chunk LDS links (option f3hl);
+                               bit 10: the general affine step on flow3 (sw_flow3a / sw_flow3ra kernels);
+                               bit 11: a flow3 column slab (peer-edge roles, sw_flow3*s_kernel);
+                               bit 12: flow3 pool loops (option f3pool);
+                               bit 13: flow3 ring at three columns per lane (sw_flow3r3 / ra3 kernels);
+                               bit 14: flow3 ring at four / five columns per lane (sw_flow3r45_kernel) */
 } sw_stats;
 int sw_last_stats(sw_stats* out);
 
