@@ -407,6 +407,33 @@ def c5_runs(sw, torch, gold, steps):
     return out
 
 
+def headline_summary(out):
+    """{workload: [ms_per_step, GCUPS, parity]} of the line's main workload and its nested extras."""
+    def row(d):
+        return [d.get("ms_per_step"), round(d["value"]) if d.get("value") is not None else None, d.get("parity")]
+    wl = (out.get("config") or {}).get("workload", "main")
+    key = "c2" if wl.startswith("C2") else "c3" if wl.startswith("C3") else "c4" if wl.startswith("C4") else \
+        "c5" if wl.startswith("C5") else "main"
+    if out.get("config", {}).get("params") == list(AFFINE_PARAMS):
+        key += "_affine"
+    res = {key: row(out)}
+    if isinstance(out.get("affine_step"), dict) and out["affine_step"].get("value") is not None:
+        res["c2_affine"] = row(out["affine_step"])
+    b = out.get("batch_c3") or out.get("batch_c4")
+    if isinstance(b, dict):
+        res["c3" if "batch_c3" in out else "c4"] = row(b)
+        if isinstance(b.get("affine_step"), dict) and b["affine_step"].get("value") is not None:
+            res["c3_affine"] = row(b["affine_step"])
+        if isinstance(b.get("int32_kernel"), dict):
+            res["c3_int32_kernel_ms"] = b["int32_kernel"].get("kernel_ms_per_launch")
+    for k in ("linear", "affine"):
+        c = (out.get("c5") or {}).get(k)
+        if isinstance(c, dict):
+            res["c5" if k == "linear" else "c5_affine"] = row(c)
+    res["units"] = "[ms_per_step, GCUPS, parity]"
+    return res
+
+
 def affine_key(st):
     """"_affine" when a launch ran the general affine step (its counter profile is
     profiles/pmc_<workload>_affine.json, tools/pmc_summary.py c2a / c3a / c5a)."""
@@ -904,6 +931,9 @@ def main():
                 out["cpu_baseline"] = cpu_baseline(workload, cfg["N"], args.cpu_seconds, params)
             except Exception as e:   # the baseline leg must not kill the GPU number
                 out["cpu_baseline"] = {"error": repr(e)}
+        # last key of the line: every workload's step time, rate and parity in a few hundred bytes, so a
+        # record that keeps only the tail of the output (the driver keeps 2000 characters) still holds them
+        out["summary"] = headline_summary(out)
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()
