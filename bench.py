@@ -277,7 +277,10 @@ def kernel_label(st):
         if f3 or aff3:
             name = ("flow3 ring" if ring else "flow3") + (" affine" if aff3 else "") + (" W3" if v & 8192 else "") + \
                 (" W4/W5" if v & 16384 else "") + (" pool loops" if v & 4096 else "")
+            if v & 32768:
+                name = "flow3 W3, pair per workgroup"
             fn = "sw_flow3p_kernel" if v & 4096 else "sw_flow3r45_kernel" if v & 16384 else \
+                "sw_flow3r3p_kernel" if v & 32768 else \
                 ("sw_flow3r" if ring else "sw_flow3") + ("a" if aff3 else "") + ("3" if v & 8192 else "") + \
                 ("s" if v & 2048 else "") + "_kernel"
             if v & 2048:
@@ -866,19 +869,23 @@ def main():
             # the same batch on the int32 kernels (no 16-bit packing): the flow2 step with a
             # pair per workgroup, which the engine picks for batches whose scores need int32,
             # and the pair-per-workgroup strip kernel it replaced there
-            for key, mode, pwg, name in (("int32_kernel", 5, 1, "flow2 pair per workgroup"),
-                                         ("pairwg_kernel", 1, -1, "pairwg")):
+            for key, mode, pwg, f3pwg, name in (("int32_kernel", 5, 1, 1, "flow3 W3 pair per workgroup"),
+                                                ("int32_flow2_kernel", 5, 1, 0, "flow2 pair per workgroup"),
+                                                ("pairwg_kernel", 1, -1, 1, "pairwg")):
                 sw.set_option("mode", mode)
                 sw.set_option("f2pwg", pwg)
+                sw.set_option("f3pwg", f3pwg)
                 try:
                     it, ik, isc, _, ist = run_batch(sw, torch, None, 1, 0, 8192, 1024, 2, 1)
-                    extra[key] = {"kernel": name, "kernel_ms_per_launch": round(ik, 4),
+                    extra[key] = {"kernel": name, "kernel_fn": kernel_label(ist)["kernel_fn"],
+                                  "kernel_ms_per_launch": round(ik, 4),
                                   "kernel_gcups": round(bcells / (ik * 1e-3) / 1e9, 3),
                                   "parity": ("ok" if isc == ref[:len(isc)] else "MISMATCH")
                                   if defaults and len(ref) >= 1024 else "unchecked"}
                 finally:
                     sw.set_option("mode", args.mode if args.mode >= 0 else -1)
                     sw.set_option("f2pwg", -1)
+                    sw.set_option("f3pwg", 1)
             if defaults and args.mode < 0:
                 extra["affine_step"] = batch_affine_runs(sw, torch, gold, bsteps, params, bcells)
 

@@ -66,7 +66,7 @@ std::atomic<long long> g_opt_W{0}, g_opt_C{0}, g_opt_bytes{0}, g_opt_timeout{30}
     g_opt_mode{-1}, g_opt_trace{0}, g_opt_duo_f16{1}, g_opt_f2stream{0}, g_opt_ring{-1}, g_opt_ring_rows{4096}, g_opt_f2_wgs{0}, g_opt_f2w{0}, g_opt_f2pwg{-1},
     g_opt_linear{-1}, g_opt_f3{1}, g_opt_slab_plain{0}, g_opt_duo_lds{1}, g_opt_duo_tab{1}, g_opt_duo_roles{1}, g_opt_f3hl{1},
     g_opt_f3rhl{0}, g_opt_f3a{1}, g_opt_f3slab{1}, g_opt_duo_prio{-1}, g_opt_f3pool{0},
-    g_opt_stall_item{-1};
+    g_opt_stall_item{-1}, g_opt_f3pwg{1};
 
 // Longest sequence the engine takes: granule buffers of m rows keep m * 16 in the
 // 32-bit record count of a buffer resource (sw_device.h linear_edge).
@@ -205,6 +205,7 @@ struct Job {
     bool f2w2 = false;           // MODE_FLOW2: two columns per lane (strips of 126 new columns, LIN step)
     bool f2w3 = false;           // ... three (strips of 189; with f2w2: flow3 ring mode only, sw_flow3r3_kernel)
     int w45_s4 = -1;             // with f2w3: four / five columns per lane instead (sw_flow3r45_kernel, plan_w45)
+    bool f3pwg = false;          // with pwg: flow3's three-column ring step, a pair per workgroup (plan_pwg3)
     bool pwg = false;            // MODE_FLOW2 batch: a pair per workgroup (sw_flow2.hip PWG)
 };
 
@@ -451,6 +452,27 @@ void plan_pwg(Job& job, const Params& prm) {
     job.f2_stream = true;
 }
 
+// A batch whose scores need int32 on flow3's three-column ring step with a pair per workgroup
+// (sw_flow3r3p_kernel): the linear-gap step only (G_INIT == G_EXT, option linear not 0), rows up to
+// 2^16 (the block's edge ring holds a whole strip edge), option f3pwg not 0.  Against flow2's PWG
+// kernel (two columns, compiled loop, 3 per CU by its round buffer): 12.5 + 1.6 instead of ~10.7
+// VALU per step for 1.5x the columns, 4 workgroups per CU (a C3-sized batch in one pass).
+bool pwg3_fits(const Job& job, const Params& prm) {
+    int max_m = 0;
+    for (const PairDesc& d : job.pairs) max_m = std::max(max_m, d.m);
+    return g_opt_f3pwg.load() != 0 && g_opt_f3.load() != 0 && job.dna && prm.gap_init == prm.gap_ext &&
+           g_opt_linear.load() != 0 && prm.match + prm.gap_init <= 127 && prm.mismatch + prm.gap_init >= -127 &&
+           max_m <= (1 << 16) && (g_opt_C.load() == 0 || g_opt_C.load() == 64) && g_opt_f2w.load() != 1 &&
+           g_opt_f2w.load() != 2;
+}
+void plan_pwg3(Job& job) {
+    job.W = 1;
+    job.C = 64;
+    plan_flow2(job, true, true, true);
+    job.f3pwg = true;
+    job.f2_stream = true;
+}
+
 // A DNA batch on the flow2 item claim: a pair's strip groups spread over many CUs (W = 1
 // strips, 64-row chunks, streamed codes, 2 workgroups per CU from 4 groups per CU).
 void plan_claim(Job& job, const Params& prm) {
@@ -475,6 +497,11 @@ int finalize_mode(Job& job, const Params& prm, int cus) {
     if (job.mode == MODE_FLOW2 && job.pairs.size() > 1 && g_opt_f2pwg.load() == 1) {
         Job w1 = job;   // a forced flow2 batch, a pair per workgroup (W = 1 strips, C = 64)
         plan(w1, 1, 64, false, MODE_FLOW2);
+        if (flow2_fits(w1, prm) && pwg3_fits(w1, prm)) {
+            job = w1;
+            plan_pwg3(job);
+            return 0;
+        }
         if (flow2_fits(w1, prm) && pwg_fits(w1, prm, 1)) {
             job = w1;
             plan_pwg(job, prm);
@@ -571,6 +598,13 @@ int finalize_mode(Job& job, const Params& prm, int cus) {
             plan_claim(job, prm);
             return 0;
         }
+        // (256 x 8192, kernel ms, flow2 PWG / flow3 PWG at three columns: 3.30 / 2.87; 384: 5.25 / 5.05;
+        // 16384 rows, 256 pairs: 12.4 / 11.1; profiles/r06_pwg3_sweep.jsonl)
+        if (f2ok && P < 2 * cus && pwg3_fits(w1, prm)) {
+            job = w1;
+            plan_pwg3(job);
+            return 0;
+        }
         if (f2ok && P < 2 * cus && pwg_fits(w1, prm, 2)) {
             job = w1;
             plan_pwg(job, prm);
@@ -586,11 +620,14 @@ int finalize_mode(Job& job, const Params& prm, int cus) {
             set_err("duo mode needs an {A,C,G,T} batch whose scores fit 16 bits (MATCH*min(n,m)+MATCH <= 65535)");
             return -1;
         }
-        // scores that need int32: the flow2 step with a pair per workgroup when its round
-        // buffer fits (C3-shaped batch on int32: pairwg 18.8 ms -> PWG 9.95 ms), else the item claim
+        // scores that need int32: flow3's three-column step with a pair per workgroup at the linear-gap
+        // step (C3-shaped batch on int32: 8.88-9.39 ms against flow2's PWG 9.70-9.88 on the same box), else
+        // the flow2 step with a pair per workgroup when its round buffer fits (pairwg 18.8 ms -> PWG 9.95
+        // ms), else the item claim
         if (f2ok) {
             job = w1;
-            if (pwg_fits(w1, prm, 2)) plan_pwg(job, prm);
+            if (pwg3_fits(w1, prm)) plan_pwg3(job);
+            else if (pwg_fits(w1, prm, 2)) plan_pwg(job, prm);
             else plan_claim(job, prm);
         }
     }
@@ -718,6 +755,7 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
         f2_wgs = o > 0           ? (int)o
                  : job.ring      ? (job.item_base[np] <= c->cus * F2_WGS_MAX || job.f2w3 ? F2_WGS_MAX
                                                                              : std::min(F2_WGS_MAX, std::max(1, per_cu / 2)))
+                 : job.f3pwg     ? std::min(F2_WGS_MAX, std::max(1, per_cu_ceil))
                  : job.pwg       ? std::min({F2_WGS_MAX, std::max(1, per_cu_ceil),
                                              flow2_pwg_wgs(max_m_all, job.C, job.f2w2)})
                  : per_cu >= 4   ? 2
@@ -824,6 +862,20 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
         if (c->cons.ensure((size_t)ring_blocks * RING_CONS_STRIDE, s)) return -1;
         HIPCHK(hipMemsetAsync(c->cons.p, 0, (size_t)ring_blocks * RING_CONS_STRIDE * sizeof(unsigned), s));
     }
+    int pwg3_blocks = 0;
+    if (job.f3pwg) {
+        // one edge ring per block (a pair's strip edge, >= max m rows); the grid: a block per pair up
+        // to f2_wgs per CU, blocks running further pairs in turn (no block waits on another)
+        if (edge != nullptr || job.ring || !job.f2w3 || !f2_lin) {
+            set_err("the pair-per-workgroup three-column kernel takes batches at the linear-gap step only");
+            return -1;
+        }
+        pwg3_blocks = (int)std::min<long long>(np, (long long)c->cus * f2_wgs);
+        if (g_opt_blocks.load() > 0) pwg3_blocks = (int)std::min<long long>(g_opt_blocks.load(), np);
+        wrap_rows = 64;
+        while (wrap_rows < max_m_all) wrap_rows *= 2;
+        job.bnd_granules = (uint64_t)pwg3_blocks * (uint64_t)wrap_rows;
+    }
     if (duo_wrap > 0 && g_opt_duo_roles.load() != 0) {   // one word per CU (XCC, SE, SH, CU of HW_ID)
         if (c->cons.ensure(DUO_CU_WORDS, s)) return -1;
         HIPCHK(hipMemsetAsync(c->cons.p, 0, DUO_CU_WORDS * sizeof(unsigned), s));
@@ -871,11 +923,13 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
     cfg.f3p = g_opt_f3pool.load() != 0 && cfg.f3_hl && job.C == 32 && !job.ring && (use_f3 || use_f3a);
     cfg.f3_w3 = job.f2w3 && job.w45_s4 < 0;
     cfg.f3_w45 = job.w45_s4 >= 0;
+    cfg.f3_pwg = job.f3pwg;
+    if (job.f3pwg) cfg.f3 = true;
     if (cfg.f3_w45 && !(use_f3 && job.ring && edge == nullptr)) {
         set_err("four / five columns per lane run on flow3's linear-gap ring kernel only (one pair, not a slab)");
         return -1;
     }
-    if (job.f2w3 && !((use_f3 || use_f3ra) && job.ring && job.C == 64 && !cfg.f3_hl)) {
+    if (job.f2w3 && !job.f3pwg && !((use_f3 || use_f3ra) && job.ring && job.C == 64 && !cfg.f3_hl)) {
         set_err("three columns per lane run on flow3's ring kernel only (linear-gap step, C = 64, whole-chunk links)");
         return -1;
     }
@@ -904,6 +958,7 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
         if (job.mode == MODE_FLOW2) blocks = std::min<long long>(blocks, (long long)c->cus * f2_wgs);
     }
     if (job.ring) blocks = ring_blocks;   // checked co-resident above
+    if (job.f3pwg) blocks = pwg3_blocks;
     cfg.blocks = (int)std::max<long long>(1, blocks);
 
     KParams kp{};
@@ -963,6 +1018,7 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
         kp.wrap_rows = wrap_rows;
         kp.ring_cons = c->cons.p;
     }
+    if (job.f3pwg) kp.wrap_rows = wrap_rows;   // each block's edge ring (kp.ring_rows stays 0)
     if (edge) {   // (flow2 then runs its slab kernel, which streams the row codes)
         kp.slab_in = edge->in;
         kp.slab_out = edge->out;
@@ -987,7 +1043,7 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
                       (cfg.f2_w2 ? 16 : 0) | (cfg.f2_pwg ? 32 : 0) | (cfg.f3 ? 64 : 0) | (cfg.duo_wrap > 0 ? 128 : 0) |
                       (cfg.duo_tab > 0 ? 256 : 0) | (cfg.f3_hl ? 512 : 0) | (cfg.f3a || cfg.f3ra ? 1024 : 0) |
                       (cfg.f3_slab ? 2048 : 0) | (cfg.f3p ? 4096 : 0) | (cfg.f3_w3 ? 8192 : 0) |
-                      (cfg.f3_w45 ? 16384 : 0);
+                      (cfg.f3_w45 ? 16384 : 0) | (cfg.f3_pwg ? 32768 : 0);
     t_stats.boundary_bytes = (long long)(job.bnd_granules * sizeof(Granule));
     c->last = s;
     return 0;
@@ -1774,6 +1830,9 @@ int sw_set_option(const char* key, long long v) {
     } else if (k == "timeout") {
         if (v < 1 || v > 3600) return -1;
         g_opt_timeout = v;
+    } else if (k == "f3pwg") {   // 1 (default): int32 batches (linear-gap step) on flow3's three-column step, a pair
+        // per workgroup (sw_flow3r3p_kernel); 0: flow2's pair-per-workgroup kernel
+        g_opt_f3pwg = v ? 1 : 0;
     } else if (k == "stall_item") {   // tests only: flow2's compute waves skip this item (-1 = none)
         if (v < -1) return -1;
         g_opt_stall_item = v;
@@ -1861,6 +1920,7 @@ long long sw_get_option(const char* key) {
     if (k == "bytes") return g_opt_bytes;
     if (k == "timeout") return g_opt_timeout;
     if (k == "stall_item") return g_opt_stall_item;
+    if (k == "f3pwg") return g_opt_f3pwg;
     if (k == "blocks") return g_opt_blocks;
     if (k == "orient") return g_opt_orient;
     if (k == "trace") return g_opt_trace;

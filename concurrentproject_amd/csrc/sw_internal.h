@@ -145,6 +145,7 @@ struct LaunchCfg {
     bool f3p = false;       // flow3 staged on the pool loops (sw_flow3p_kernel: C = 32, f3_hl, no I/O rotation)
     bool f3_w3 = false;     // flow3 ring mode at three columns per lane (sw_flow3r3_kernel / sw_flow3r3s_kernel)
     bool f3_w45 = false;    // flow3 ring mode at four and five columns per lane (sw_flow3r45_kernel, KParams::w45_s4)
+    bool f3_pwg = false;    // flow3 three-column ring step, a pair per workgroup (sw_flow3r3p_kernel; int32 batches)
     bool f3ra = false;      // MODE_FLOW2 ring-mode two-column launch with the affine step on flow3 (sw_flow3ra_kernel)
     bool f3_slab = false;   // flow3 ring launch of a column slab (sw_flow3rs_kernel / sw_flow3ras_kernel)
     int duo_wrap = 0;       // MODE_DUO at C = 64: > 0 = strip hand-offs in LDS (sw_duo_lds_kernel), this many
