@@ -40,6 +40,7 @@ def _defaults(engine):
         engine.set_option("linear", -1)
         engine.set_option("f2w", 0)
         engine.set_option("f2pwg", -1)
+        engine.set_option("f3pwg", 1)
     reset()
     yield
     reset()
@@ -52,13 +53,15 @@ SHAPES = [(1, 1), (5, 200), (128, 64), (129, 63), (254, 65), (255, 129), (504, 1
 
 
 def test_pwg_forced_matches_oracle(engine, oracle_mod):
-    """f2pwg = 1 with mode 5: ragged batch, linear-gap and affine constants, the
-    automatic grid and grids of 1 and 3 workgroups (each runs many pairs)."""
+    """f2pwg = 1 with mode 5 on flow2's kernel (f3pwg = 0; flow3's three-column one: test_pwg3.py):
+    ragged batch, linear-gap and affine constants, the automatic grid and grids of 1 and 3 workgroups
+    (each runs many pairs)."""
     rng = np.random.default_rng(21)
     pairs = _pairs(rng, SHAPES)
     engine.set_option("orient", 1)
     engine.set_option("mode", 5)
     engine.set_option("f2pwg", 1)
+    engine.set_option("f3pwg", 0)
     for prm in (engine.Params(), engine.Params(2, -3, 5, 2), engine.Params(3, -2, 4, 4), engine.Params(1, 0, 0, 0)):
         op = oracle_mod.Params(prm.match, prm.mismatch, prm.gap_init, prm.gap_ext)
         exp = [oracle_mod.score_linear(a, b, op) for a, b in pairs]
@@ -136,6 +139,7 @@ def test_pwg_config_c3_on_int32(engine, golden):
     s = torch.cuda.current_stream()
     engine.set_option("mode", 5)
     engine.set_option("f2pwg", 1)
+    engine.set_option("f3pwg", 0)   # flow2's kernel (flow3's: test_pwg3.py)
     engine.score_batch_device(arena.data_ptr(), [2 * N * k for k in range(P)], [N] * P,
                               [2 * N * k + N for k in range(P)], [N] * P, scores.data_ptr(), flags=1,
                               stream=s.cuda_stream)
