@@ -1,4 +1,4 @@
-"""CPU: every committed bench line of this round (profiles/r05*_bench_*.json) carries a
+"""CPU: every committed bench line of this round (profiles/r06*_bench_*.json) carries a
 counter-derived roofline whose `frac` / `achieved` match the profiles/pmc_*.json it names
 (same sha256) to 3 digits, and whose config.kernel_fn is the kernel that profile counted
 (tools/check_bench_lines.py, strict mode)."""

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Check committed bench lines against the counter profiles they were computed from.
 
-    python tools/check_bench_lines.py [profiles/r05*_bench_*.json ...]
+    python tools/check_bench_lines.py [profiles/r06*_bench_*.json ...]
 
 For every bench JSON line (the top-level roofline and the nested batch_c3 / batch_c4
 rooflines) whose roofline names a profiles/pmc_*.json and carries its sha256
@@ -42,6 +42,9 @@ def rooflines(line):
         sub = line.get(key)
         if isinstance(sub, dict) and "roofline" in sub:
             yield key, sub["roofline"], sub["kernel_ms_per_launch"], sub.get("kernel_fn")
+        aff = (sub or {}).get("affine_step") if key != "affine_step" and isinstance(sub, dict) else None
+        if isinstance(aff, dict) and "roofline" in aff:
+            yield key + ".affine_step", aff["roofline"], aff["kernel_ms_per_launch"], aff.get("kernel_fn")
     for key in ("linear", "affine"):
         sub = (line.get("c5") or {}).get(key)
         if isinstance(sub, dict) and "roofline" in sub:
@@ -85,7 +88,7 @@ def check(path, strict):
 def main():
     args = sys.argv[1:]
     strict = not args
-    paths = args or sorted(glob.glob(os.path.join(ROOT, "profiles", "r05*_bench_*.json")))
+    paths = args or sorted(glob.glob(os.path.join(ROOT, "profiles", "r06*_bench_*.json")))
     bad = []
     for p in paths:
         bad += check(p, strict)
