@@ -278,9 +278,9 @@ def kernel_label(st):
             name = ("flow3 ring" if ring else "flow3") + (" affine" if aff3 else "") + (" W3" if v & 8192 else "") + \
                 (" W4/W5" if v & 16384 else "") + (" pool loops" if v & 4096 else "")
             if v & 32768:
-                name = "flow3 W3, pair per workgroup"
+                name = "flow3 W3%s, pair per workgroup" % (" affine" if aff3 else "")
             fn = "sw_flow3p_kernel" if v & 4096 else "sw_flow3r45_kernel" if v & 16384 else \
-                "sw_flow3r3p_kernel" if v & 32768 else \
+                ("sw_flow3ra3p_kernel" if aff3 else "sw_flow3r3p_kernel") if v & 32768 else \
                 ("sw_flow3r" if ring else "sw_flow3") + ("a" if aff3 else "") + ("3" if v & 8192 else "") + \
                 ("s" if v & 2048 else "") + "_kernel"
             if v & 2048:

@@ -457,11 +457,15 @@ void plan_pwg(Job& job, const Params& prm) {
 // 2^16 (the block's edge ring holds a whole strip edge), option f3pwg not 0.  Against flow2's PWG
 // kernel (two columns, compiled loop, 3 per CU by its round buffer): 12.5 + 1.6 instead of ~10.7
 // VALU per step for 1.5x the columns, 4 workgroups per CU (a C3-sized batch in one pass).
-bool pwg3_fits(const Job& job, const Params& prm) {
+// The general affine step takes the same organisation on the three-column affine ring step
+// (sw_flow3ra3p_kernel, option f3a not 0) where `affine` allows it: C3-shaped at (2, -3, 5, 2) on int32
+// flow2's PWG (one column per lane) runs 21.1 ms.
+bool pwg3_fits(const Job& job, const Params& prm, bool affine = false) {
     int max_m = 0;
     for (const PairDesc& d : job.pairs) max_m = std::max(max_m, d.m);
-    return g_opt_f3pwg.load() != 0 && g_opt_f3.load() != 0 && job.dna && prm.gap_init == prm.gap_ext &&
-           g_opt_linear.load() != 0 && prm.match + prm.gap_init <= 127 && prm.mismatch + prm.gap_init >= -127 &&
+    const bool lin = prm.gap_init == prm.gap_ext && g_opt_linear.load() != 0;
+    return g_opt_f3pwg.load() != 0 && job.dna && (lin ? g_opt_f3.load() != 0 : affine && g_opt_f3a.load() != 0) &&
+           prm.match + prm.gap_init <= 127 && prm.mismatch + prm.gap_init >= -127 &&
            max_m <= (1 << 16) && (g_opt_C.load() == 0 || g_opt_C.load() == 64) && g_opt_f2w.load() != 1 &&
            g_opt_f2w.load() != 2;
 }
@@ -497,7 +501,7 @@ int finalize_mode(Job& job, const Params& prm, int cus) {
     if (job.mode == MODE_FLOW2 && job.pairs.size() > 1 && g_opt_f2pwg.load() == 1) {
         Job w1 = job;   // a forced flow2 batch, a pair per workgroup (W = 1 strips, C = 64)
         plan(w1, 1, 64, false, MODE_FLOW2);
-        if (flow2_fits(w1, prm) && pwg3_fits(w1, prm)) {
+        if (flow2_fits(w1, prm) && pwg3_fits(w1, prm, true)) {
             job = w1;
             plan_pwg3(job);
             return 0;
@@ -626,7 +630,7 @@ int finalize_mode(Job& job, const Params& prm, int cus) {
         // ms), else the item claim
         if (f2ok) {
             job = w1;
-            if (pwg3_fits(w1, prm)) plan_pwg3(job);
+            if (pwg3_fits(w1, prm, true)) plan_pwg3(job);
             else if (pwg_fits(w1, prm, 2)) plan_pwg(job, prm);
             else plan_claim(job, prm);
         }
@@ -763,7 +767,8 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
     }
     // G_INIT == G_EXT: the exact linear-gap step (sw_flow2.hip LIN), unless disabled; the
     // pair-per-workgroup kernel is built with it exactly at two columns per lane
-    const bool f2_lin = job.pwg ? job.f2w2
+    const bool f2_lin = job.f3pwg ? prm.gap_init == prm.gap_ext && g_opt_linear.load() != 0
+                      : job.pwg   ? job.f2w2
                                 : ((job.mode == MODE_FLOW2 &&
                                     (job.C == 32 || job.C == 64 || (job.C == 16 && job.f2w2))) ||
                                    (job.mode == MODE_DUO && job.duo_f16)) &&
@@ -866,8 +871,8 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
     if (job.f3pwg) {
         // one edge ring per block (a pair's strip edge, >= max m rows); the grid: a block per pair up
         // to f2_wgs per CU, blocks running further pairs in turn (no block waits on another)
-        if (edge != nullptr || job.ring || !job.f2w3 || !f2_lin) {
-            set_err("the pair-per-workgroup three-column kernel takes batches at the linear-gap step only");
+        if (edge != nullptr || job.ring || !job.f2w3) {
+            set_err("the pair-per-workgroup three-column kernel takes batches only");
             return -1;
         }
         pwg3_blocks = (int)std::min<long long>(np, (long long)c->cus * f2_wgs);
@@ -924,7 +929,10 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
     cfg.f3_w3 = job.f2w3 && job.w45_s4 < 0;
     cfg.f3_w45 = job.w45_s4 >= 0;
     cfg.f3_pwg = job.f3pwg;
-    if (job.f3pwg) cfg.f3 = true;
+    if (job.f3pwg) {   // the linear-gap ring step, or the affine one (sw_flow3ra3p_kernel)
+        cfg.f3 = f2_lin;
+        cfg.f3ra = !f2_lin;
+    }
     if (cfg.f3_w45 && !(use_f3 && job.ring && edge == nullptr)) {
         set_err("four / five columns per lane run on flow3's linear-gap ring kernel only (one pair, not a slab)");
         return -1;
@@ -939,7 +947,7 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
         set_err("flow2: two columns per lane at C = 16 runs on flow3 only (rows staged in LDS, one GPU)");
         return -1;
     }
-    if (cfg.f2_w2 && !f2_lin && !use_f3ra) {   // the strips were cut for two columns per lane
+    if (cfg.f2_w2 && !f2_lin && !use_f3ra && !job.f3pwg) {   // the strips were cut for two columns per lane
         set_err("flow2: two columns per lane needs the linear-gap step (or flow3's affine ring kernel)");
         return -1;
     }
@@ -1830,8 +1838,8 @@ int sw_set_option(const char* key, long long v) {
     } else if (k == "timeout") {
         if (v < 1 || v > 3600) return -1;
         g_opt_timeout = v;
-    } else if (k == "f3pwg") {   // 1 (default): int32 batches (linear-gap step) on flow3's three-column step, a pair
-        // per workgroup (sw_flow3r3p_kernel); 0: flow2's pair-per-workgroup kernel
+    } else if (k == "f3pwg") {   // 1 (default): int32 batches on flow3's three-column ring step, a pair per
+        // workgroup (sw_flow3r3p_kernel, affine: sw_flow3ra3p_kernel); 0: flow2's pair-per-workgroup kernel
         g_opt_f3pwg = v ? 1 : 0;
     } else if (k == "stall_item") {   // tests only: flow2's compute waves skip this item (-1 = none)
         if (v < -1) return -1;

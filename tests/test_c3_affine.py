@@ -47,13 +47,20 @@ def _auto_plan(engine, pairs, prm, want):
 
 
 def _int32_plan(engine, pairs, prm, want, pwg):
+    """The int32 kernels: flow3's three-column affine ring step with a pair per workgroup (f3pwg 1,
+    variant 32768) and flow2's one-column step (f3pwg 0)."""
     engine.set_option("mode", 5)
     engine.set_option("f2pwg", pwg)
-    got = engine.score_batch(pairs, prm)
-    st = engine.last_stats()
-    assert st["mode"] == 5 and not st["variant"] & 8, st
-    bad = [k for k in range(len(want)) if got[k] != want[k]]
-    assert not bad, ("int32 affine", pwg, bad[:8])
+    try:
+        for f3pwg in (1, 0):
+            engine.set_option("f3pwg", f3pwg)
+            got = engine.score_batch(pairs, prm)
+            st = engine.last_stats()
+            assert st["mode"] == 5 and not st["variant"] & 8 and bool(st["variant"] & 32768) == bool(f3pwg), st
+            bad = [k for k in range(len(want)) if got[k] != want[k]]
+            assert not bad, ("int32 affine", pwg, f3pwg, bad[:8])
+    finally:
+        engine.set_option("f3pwg", 1)
 
 
 def test_c3_affine_golden(engine, golden):

@@ -37,7 +37,8 @@ def _forced(engine):
 def test_pwg3_ragged_parity(engine, oracle_mod):
     """Ragged pairs around the 189-column strips, the 756-column groups and the 64-row chunks (one to
     nine groups per pair, rows 1..3000), on grids of 1, 3 and 7 workgroups (workgroups running several
-    pairs in turn) and the automatic grid; the default and two other linear-gap constant sets."""
+    pairs in turn) and the automatic grid; three linear-gap constant sets and three affine ones
+    (G_INIT > G_EXT, G_INIT < G_EXT) on the affine ring step."""
     rng = np.random.default_rng(33)
     shapes = [(1, 1), (5, 300), (192, 64), (193, 65), (380, 129), (756, 700), (757, 1000), (1513, 63),
               (2000, 2049), (3000, 511), (4000, 1500), (6805, 3000), (300, 1)]
@@ -47,14 +48,17 @@ def test_pwg3_ragged_parity(engine, oracle_mod):
         pairs.append((a, _similar(rng, a, m)) if m > 10 and rng.random() < 0.6 else (a, _rand_dna(rng, m)))
     engine.set_option("orient", 1)
     _forced(engine)
-    for prm in ((1, -1, 1, 1), (2, -3, 2, 2), (3, 0, 4, 4)):
+    for prm in ((1, -1, 1, 1), (2, -3, 2, 2), (3, 0, 4, 4), (2, -3, 5, 2), (1, -1, 3, 1), (1, -1, 1, 3)):
         p = engine.Params(*prm)
         exp = [oracle_mod.score_linear(a, b, oracle_mod.Params(*prm)) for a, b in pairs]
         for blocks in (1, 3, 7, 0):
             engine.set_option("blocks", blocks)
             got = engine.score_batch(pairs, p)
             st = engine.last_stats()
-            assert st["mode"] == 5 and st["variant"] & PWG3 and st["variant"] & 8, (prm, blocks, st)
+            lin = prm[2] == prm[3]
+            # the linear-gap ring step (variant 8) or the affine one (1024: sw_flow3ra3p_kernel)
+            assert st["mode"] == 5 and st["variant"] & PWG3, (prm, blocks, st)
+            assert bool(st["variant"] & 8) == lin and bool(st["variant"] & 1024) == (not lin), (prm, st)
             assert got == exp, (prm, blocks, [(k, got[k], exp[k]) for k in range(len(exp)) if got[k] != exp[k]][:5])
 
 
@@ -94,4 +98,22 @@ def test_pwg3_automatic_int32_batch(engine, oracle_mod):
         assert got[k] == oracle_mod.score_linear(pairs[k][0], pairs[k][1], op), k
     engine.set_option("f3pwg", 0)
     assert engine.score_batch(pairs, p) == got
+    assert not engine.last_stats()["variant"] & PWG3
+
+
+def test_pwg3_affine_c3_golden(engine, golden):
+    """C3 at (2, -3, 5, 2) forced onto the int32 kernels (its scores fit 16 bits): flow3's three-column
+    affine pair-per-workgroup kernel and flow2's one-column one both give C3_affine (the reference's
+    refvar LazySmith)."""
+    c = golden("configs.json")["C3_affine"]
+    N = c["N"]
+    arena = engine.gen_batch(c["seed_base"], c["npairs"], N)
+    pairs = [(arena[2 * N * k:2 * N * k + N], arena[2 * N * k + N:2 * N * (k + 1)]) for k in range(c["npairs"])]
+    p = engine.Params(*c["params"])
+    _forced(engine)
+    assert engine.score_batch(pairs, p) == c["scores"]
+    st = engine.last_stats()
+    assert st["variant"] & PWG3 and st["variant"] & 1024 and not st["variant"] & 8, st
+    engine.set_option("f3pwg", 0)
+    assert engine.score_batch(pairs, p) == c["scores"]
     assert not engine.last_stats()["variant"] & PWG3
