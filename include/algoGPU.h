@@ -216,6 +216,8 @@ void sw_db_close(sw_db* db);
  *              0 = (default) whole-chunk links (measured faster on C5)
  *   "f3a"      1 = (default) the general affine step runs on flow3 (staged: sw_flow3a_kernel, one
  *              column per lane, C2 with G_INIT != G_EXT; ring: sw_flow3ra(3)_kernel, C5), 0 = flow2
+ *   "f3pwg"    1 = (default) DNA batches on a pair-per-workgroup plan (scores that need int32, or 1-2
+ *              pairs per CU) run flow3's three-column ring step (sw_flow3r3p / ra3p_kernel), 0 = flow2's
  *   "f3slab"   1 = (default) column slabs run flow3's ring kernel with slab roles
  *              (sw_flow3rs / ras / r3s / ra3s_kernel), 0 = flow2's slab kernel
  *   "duo_lds"  1 = (default) duo batches at C = 64 hand strip edges on in LDS when a round's
@@ -257,7 +259,9 @@ typedef struct {
                                bit 11: a flow3 column slab (peer-edge roles, sw_flow3*s_kernel);
                                bit 12: flow3 pool loops (option f3pool);
                                bit 13: flow3 ring at three columns per lane (sw_flow3r3 / ra3 kernels);
-                               bit 14: flow3 ring at four / five columns per lane (sw_flow3r45_kernel) */
+                               bit 14: flow3 ring at four / five columns per lane (sw_flow3r45_kernel);
+                               bit 15: flow3 three-column ring step with a pair per workgroup
+                                       (sw_flow3r3p_kernel / sw_flow3ra3p_kernel: int32 batches) */
 } sw_stats;
 int sw_last_stats(sw_stats* out);
 
