@@ -262,10 +262,8 @@ def test_flow3ra_config_c5_affine_similar(engine, golden, oracle_mod):
     """An E/F-heavy pair at C5 size (oracle.similar_pair(20, 2^20), alignments of ~1.5M with
     indels of up to 4096 bases) at (2, -3, 5, 2) on the default plan (flow3 W3 ring affine),
     against C5_affine_similar (the oracle's pthread wavefront and the reference's LazySmith)."""
-    cfg = golden("configs.json")
-    if "C5_affine_similar" not in cfg:
-        pytest.skip("C5_affine_similar not pinned yet (tests/golden/gen_pin.py --c5similar)")
-    g = cfg["C5_affine_similar"]
+    g = golden("configs.json")["C5_affine_similar"]
+    assert any(p.startswith("reference LazySmith") for p in g["pinned_by"]), g["pinned_by"]
     a, b = oracle_mod.similar_pair(20, g["N"])
     engine.set_params(engine.Params(*g["params"]))
     assert _device_score(engine, a, b) == g["score"]

@@ -168,3 +168,18 @@ def test_config_c5_affine_fixture(oracle_mod, golden):
     for eng in ("ref", "wavefront"):
         r = golden("c5_affine_%s.json" % eng)
         assert r["score"] == c["score"] and r["sha256"] == c["sha256"] and r["params"] == c["params"], (eng, r)
+
+
+def test_config_c5_affine_similar_fixture(oracle_mod, golden):
+    """The E/F-heavy C5-size golden: oracle.similar_pair(20, 2^20) at (2, -3, 5, 2), scored
+    1392524 by the reference's own LazySmith built with those constants (1 thread, 2.8 h) and by
+    the oracle's wavefront restatement (tests/golden/gen_pin.py --c5similar); both result files
+    are committed and name the same pair."""
+    c = golden("configs.json")["C5_affine_similar"]
+    a, b = oracle_mod.similar_pair(20, c["N"])
+    assert _sha(a, b) == c["sha256"] and c["params"] == [2, -3, 5, 2]
+    assert any("reference LazySmith" in s for s in c["pinned_by"]), c["pinned_by"]
+    assert any("swo_wavefront" in s for s in c["pinned_by"]), c["pinned_by"]
+    for eng in ("ref", "wavefront"):
+        r = golden("c5_affine_similar_%s.json" % eng)
+        assert r["score"] == c["score"] and r["sha256"] == c["sha256"] and r["params"] == c["params"], (eng, r)
