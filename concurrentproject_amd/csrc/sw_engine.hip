@@ -66,7 +66,7 @@ std::atomic<long long> g_opt_W{0}, g_opt_C{0}, g_opt_bytes{0}, g_opt_timeout{30}
     g_opt_mode{-1}, g_opt_trace{0}, g_opt_duo_f16{1}, g_opt_f2stream{0}, g_opt_ring{-1}, g_opt_ring_rows{4096}, g_opt_f2_wgs{0}, g_opt_f2w{0}, g_opt_f2pwg{-1},
     g_opt_linear{-1}, g_opt_f3{1}, g_opt_slab_plain{0}, g_opt_duo_lds{1}, g_opt_duo_tab{1}, g_opt_duo_roles{1}, g_opt_f3hl{1},
     g_opt_f3rhl{0}, g_opt_f3a{1}, g_opt_f3slab{1}, g_opt_duo_prio{-1}, g_opt_f3pool{0},
-    g_opt_stall_item{-1}, g_opt_f3pwg{1};
+    g_opt_stall_item{-1}, g_opt_f3pwg{1}, g_opt_duo_raw{1};
 
 // Longest sequence the engine takes: granule buffers of m rows keep m * 16 in the
 // 32-bit record count of a buffer resource (sw_device.h linear_edge).
@@ -284,9 +284,18 @@ void plan(Job& job, int W, int C, bool single, int mode = -1) {
     job.cells = cells;
 }
 
+// Byte batches (any byte value) on the duo kernels with the penalty from the bytes (sw_kernels.hip
+// SENT_RAW): its sentinel encoding needs MATCH - MISMATCH <= 127 and MISMATCH < 0 (dead and sentinel
+// cells then score as mismatches, below the true maximum).  Option duo_raw = 0 keeps such batches on
+// the byte-path strip kernels.
+bool duo_raw_ok(const Params& p) {
+    return g_opt_duo_raw.load() != 0 && p.mismatch < 0 && p.match - p.mismatch <= 127;
+}
+
 // Packed-u16 duo mode: exact when every H + MATCH fits 16 bits (H <= MATCH*min(n,m)).
 bool duo_fits(const Job& job, const Params& p) {
-    if (!job.dna || p.gap_init + p.match > 65535 || p.gap_ext > 65535 || p.match - p.mismatch > 254) return false;
+    if ((!job.dna && !duo_raw_ok(p)) || p.gap_init + p.match > 65535 || p.gap_ext > 65535 || p.match - p.mismatch > 254)
+        return false;
     for (auto& d : job.pairs)
         if ((long long)std::max(p.match, 1) * std::min(d.n, d.m) + p.match > 65535) return false;
     return true;
@@ -621,7 +630,8 @@ int finalize_mode(Job& job, const Params& prm, int cus) {
             return 0;
         }
         if (forced_duo) {
-            set_err("duo mode needs an {A,C,G,T} batch whose scores fit 16 bits (MATCH*min(n,m)+MATCH <= 65535)");
+            set_err("duo mode needs a batch whose scores fit 16 bits (MATCH*min(n,m)+MATCH <= 65535) and, for bytes "
+                    "outside {A,C,G,T}, MISMATCH < 0 and MATCH - MISMATCH <= 127");
             return -1;
         }
         // scores that need int32: flow3's three-column step with a pair per workgroup at the linear-gap
@@ -1841,6 +1851,9 @@ int sw_set_option(const char* key, long long v) {
     } else if (k == "f3pwg") {   // 1 (default): int32 batches on flow3's three-column ring step, a pair per
         // workgroup (sw_flow3r3p_kernel, affine: sw_flow3ra3p_kernel); 0: flow2's pair-per-workgroup kernel
         g_opt_f3pwg = v ? 1 : 0;
+    } else if (k == "duo_raw") {   // 1 (default): byte batches on the duo kernels (RAW penalty), 0: byte strip kernels
+        if (v < 0 || v > 1) return -1;
+        g_opt_duo_raw = v;
     } else if (k == "stall_item") {   // tests only: flow2's compute waves skip this item (-1 = none)
         if (v < -1) return -1;
         g_opt_stall_item = v;
@@ -1929,6 +1942,7 @@ long long sw_get_option(const char* key) {
     if (k == "timeout") return g_opt_timeout;
     if (k == "stall_item") return g_opt_stall_item;
     if (k == "f3pwg") return g_opt_f3pwg;
+    if (k == "duo_raw") return g_opt_duo_raw;
     if (k == "blocks") return g_opt_blocks;
     if (k == "orient") return g_opt_orient;
     if (k == "trace") return g_opt_trace;

@@ -672,6 +672,25 @@ __device__ __forceinline__ u16x2 vmax3h(u16x2 a, u16x2 b, u16x2 c) {
 
 constexpr unsigned SENT_DUO = 0x0C0D0C0Du;   // selector 13 in both halves -> penalty 0xFF
 
+// RAW: batches of any byte values (main.cpp:28-33 compares raw bytes; sw_engine.hip duo_fits)
+// on the same step, the penalty taken from the bytes instead of a 2-bit code and a profile.
+// A row word holds byte << 8 in each half (0x00FF for rows below 0 or past m), a column word
+// byte << 8 (0x007F past n), and pen = min(row ^ col, MATCH - MISMATCH) per half (one XOR and
+// one v_pk_min_u16 where the DNA step has one v_perm_b32):
+//   equal bytes            0
+//   different bytes        row ^ col >= 256            -> MATCH - MISMATCH
+//   sentinel row, any col  low byte 0xFF ^ (0 or 0x7F)  -> MATCH - MISMATCH
+//   live row, dead col     low byte 0x7F = 127          -> MATCH - MISMATCH
+// with MATCH - MISMATCH <= 127 (host).  Sentinel and dead cells thus score as mismatches; with
+// MISMATCH < 0 (host) each such t = H_diag + MISMATCH < H_diag, and every such H is below the
+// cells it derives from, so they stay below the true maximum as the DNA path's penalty 255 keeps
+// them (and the rows above row 0 keep H = 0: t = sat(MATCH - pen) = 0).
+constexpr unsigned SENT_RAW = 0x00FF00FFu;
+__device__ __forceinline__ u16x2 vmin2(u16x2 a, u16x2 b) { return __builtin_elementwise_min(a, b); }
+__device__ __forceinline__ unsigned col_raw(const unsigned char* c, int col, int n) {
+    return col < n ? (unsigned)c[col] << 8 : 0x7Fu;
+}
+
 __device__ __forceinline__ DuoDesc load_duo(const KParams& kp, int idx) {
     const DuoDesc raw = kp.duos[idx];
     DuoDesc d;
@@ -701,22 +720,21 @@ __device__ __forceinline__ DuoDesc load_duo(const KParams& kp, int idx) {
 #define SW_DUO_UNROLL 64
 #endif
 
-template <int W, bool M3, bool LIN = false>
-struct StripDuo {
-    unsigned pA[W], pB[W];                   // column penalty words: pair 0 (perm src1), pair 1 (perm src0)
-    u16x2 aA[W], aB[W];                      // A = H + MATCH, ping-pong (diagonal source)
-    u16x2 hg[W], eh[W], fh[W];               // saturated H-G_INIT, E-G_EXT, F-G_EXT
-    unsigned r[W];                           // row-code perm selectors
-    u16x2 L0, M;
-    unsigned IOA, IOE, IOR;
-
-    __device__ __forceinline__ void setup(const KParams& kp, const DuoDesc& d, int strip, int lane) {
-        constexpr int SW = 64 * W;
-        const unsigned char* c0 = kp.seq + d.col_off[0];
-        const unsigned char* c1 = kp.seq + d.col_off[1];
+// the column words of a duo strip's W positions: DNA penalty profiles (pA: pair 0, pB: pair 1)
+// or, RAW, the two pairs' column bytes in one word (pA; pB unused)
+template <int W, bool RAW>
+__device__ __forceinline__ void duo_columns(const KParams& kp, const DuoDesc& d, int strip, int lane, unsigned (&pA)[W],
+                                            unsigned (&pB)[W]) {
+    constexpr int SW = 64 * W;
+    const unsigned char* c0 = kp.seq + d.col_off[0];
+    const unsigned char* c1 = kp.seq + d.col_off[1];
 #pragma unroll
-        for (int p = 0; p < W; ++p) {
-            const int c = strip * SW + lane * W + p;
+    for (int p = 0; p < W; ++p) {
+        const int c = strip * SW + lane * W + p;
+        if constexpr (RAW) {
+            pA[p] = col_raw(c0, c, d.n[0]) | (col_raw(c1, c, d.n[1]) << 16);
+            pB[p] = 0u;
+        } else {
             unsigned w0 = 0xFFFFFFFFu, w1 = 0xFFFFFFFFu;   // dead column: penalty 255 for every row code
             if (c < d.n[0]) {
                 const int q = dna_code(c0[c]);
@@ -729,12 +747,35 @@ struct StripDuo {
             pA[p] = w0;
             pB[p] = w1;
         }
+    }
+}
+
+// the penalty MATCH - s of one position for both pairs (RAW: see SENT_RAW)
+template <bool RAW>
+__device__ __forceinline__ u16x2 duo_pen(unsigned pA, unsigned pB, unsigned rL, u16x2 P2) {
+    if constexpr (RAW) return vmin2(as16(rL ^ pA), P2);
+    else return as16(__builtin_amdgcn_perm(pB, pA, rL));
+}
+
+template <int W, bool M3, bool LIN = false, bool RAW = false>
+struct StripDuo {
+    static constexpr unsigned SENT = RAW ? SENT_RAW : SENT_DUO;
+    unsigned pA[W], pB[W];                   // column penalty words: pair 0 (perm src1), pair 1 (perm src0)
+    u16x2 aA[W], aB[W];                      // A = H + MATCH, ping-pong (diagonal source)
+    u16x2 hg[W], eh[W], fh[W];               // saturated H-G_INIT, E-G_EXT, F-G_EXT
+    unsigned r[W];                           // row-code perm selectors (RAW: row bytes)
+    u16x2 L0, M, P2;                         // P2: MATCH - MISMATCH in both halves (RAW)
+    unsigned IOA, IOE, IOR;
+
+    __device__ __forceinline__ void setup(const KParams& kp, const DuoDesc& d, int strip, int lane) {
+        duo_columns<W, RAW>(kp, d, strip, lane, pA, pB);
         const u16x2 ma2 = splat2(kp.match);
+        P2 = splat2(kp.match - kp.mismatch);
 #pragma unroll
         for (int p = 0; p < W; ++p) {   // border: H = E = F = 0
-            aA[p] = ma2; aB[p] = ma2; hg[p] = splat2(0); eh[p] = splat2(0); fh[p] = splat2(0); r[p] = SENT_DUO;
+            aA[p] = ma2; aB[p] = ma2; hg[p] = splat2(0); eh[p] = splat2(0); fh[p] = splat2(0); r[p] = SENT;
         }
-        L0 = ma2; M = splat2(0); IOA = as32(ma2); IOE = 0u; IOR = SENT_DUO;
+        L0 = ma2; M = splat2(0); IOA = as32(ma2); IOE = 0u; IOR = SENT;
     }
 
     // One anti-diagonal step; S = the step's index mod W.  Position p's row code lives
@@ -758,7 +799,7 @@ struct StripDuo {
             const u16x2 hgL = p > 0 ? hg[q] : hgL0;   // E+ = sat(H_left - G)
             const unsigned rL = r[(p + W - S % W) % W];
             const u16x2 aD = p > 0 ? aCur[q] : L0;
-            const u16x2 pen = as16(__builtin_amdgcn_perm(pB[p], pA[p], rL));
+            const u16x2 pen = duo_pen<RAW>(pA[p], pB[p], rL, P2);
             const u16x2 t = vsubs2(aD, pen);
             u16x2 H;
             if constexpr (M3) {
@@ -799,7 +840,7 @@ struct StripDuo {
             const u16x2 ehL = p > 0 ? eh[q] : ehL0;
             const unsigned rL = r[(p + W - S % W) % W];
             const u16x2 aD = p > 0 ? aCur[q] : L0;
-            const u16x2 pen = as16(__builtin_amdgcn_perm(pB[p], pA[p], rL));
+            const u16x2 pen = duo_pen<RAW>(pA[p], pB[p], rL, P2);
             const u16x2 t = vsubs2(aD, pen);                 // max(H_diag + s, 0)
             const u16x2 E = vmax2(ehL, hgL);
             const u16x2 F = vmax2(fh[p], hg[p]);
@@ -865,36 +906,20 @@ struct StripDuo {
 // position p at chunk step K lives in R[(K - p) & 15]: a code enters at position 0 and
 // stays in its register for the W steps it takes to cross the lane; the read for steps
 // K+5..K+8 is issued at step K, into registers whose codes left the lane by step K-1.
-template <int W, bool M3, bool LIN>
+template <int W, bool M3, bool LIN, bool RAW = false>
 struct StripDuoT {
     static_assert(W % 4 == 0 && W <= 8, "16-B table reads per 4 steps; a code lives W steps in 16 registers");
     unsigned pA[W], pB[W];
     u16x2 aA[W], aB[W];
     u16x2 hg[W], eh[W], fh[W];
     unsigned R[16];
-    u16x2 L0, M;
+    u16x2 L0, M, P2;
     unsigned IOA, IOE;
     const unsigned* tl;
 
     __device__ __forceinline__ void setup(const KParams& kp, const DuoDesc& d, int strip, int lane, const unsigned* tab) {
-        constexpr int SW = 64 * W;
-        const unsigned char* c0 = kp.seq + d.col_off[0];
-        const unsigned char* c1 = kp.seq + d.col_off[1];
-#pragma unroll
-        for (int p = 0; p < W; ++p) {
-            const int c = strip * SW + lane * W + p;
-            unsigned w0 = 0xFFFFFFFFu, w1 = 0xFFFFFFFFu;
-            if (c < d.n[0]) {
-                const int q = dna_code(c0[c]);
-                w0 = q == 0 ? kp.pen[0] : q == 1 ? kp.pen[1] : q == 2 ? kp.pen[2] : kp.pen[3];
-            }
-            if (c < d.n[1]) {
-                const int q = dna_code(c1[c]);
-                w1 = q == 0 ? kp.pen[0] : q == 1 ? kp.pen[1] : q == 2 ? kp.pen[2] : kp.pen[3];
-            }
-            pA[p] = w0;
-            pB[p] = w1;
-        }
+        duo_columns<W, RAW>(kp, d, strip, lane, pA, pB);
+        P2 = splat2(kp.match - kp.mismatch);
         const u16x2 ma2 = splat2(kp.match);
 #pragma unroll
         for (int p = 0; p < W; ++p) {
@@ -929,7 +954,7 @@ struct StripDuoT {
             const u16x2 hgL = p > 0 ? hg[q] : hgL0;
             const unsigned rL = R[(K - p + 16) & 15];
             const u16x2 aD = p > 0 ? aCur[q] : L0;
-            const u16x2 pen = as16(__builtin_amdgcn_perm(pB[p], pA[p], rL));
+            const u16x2 pen = duo_pen<RAW>(pA[p], pB[p], rL, P2);
             const u16x2 t = vsubs2(aD, pen);
             u16x2 H;
             if constexpr (LIN) {
@@ -1002,16 +1027,29 @@ __device__ __forceinline__ unsigned codes_duo(unsigned raw0, unsigned raw1, int 
     return 0x0C000C00u | (s1 << 16) | s0;
 }
 
+// the row word of row k0 + lane for both pairs: DNA perm selectors, or RAW bytes (SENT_RAW)
+template <bool RAW>
+__device__ __forceinline__ unsigned codes_duo_t(unsigned raw0, unsigned raw1, int k0, int lane, int C, const DuoDesc& d) {
+    if constexpr (RAW) {
+        const int row = k0 + lane;
+        const bool l0 = lane < C && row >= 0 && row < d.m[0];
+        const bool l1 = lane < C && row >= 0 && row < d.m[1];
+        return (l0 ? (raw0 & 0xFFu) << 8 : 0xFFu) | ((l1 ? (raw1 & 0xFFu) << 8 : 0xFFu) << 16);
+    } else {
+        return codes_duo(raw0, raw1, k0, lane, C, d);
+    }
+}
+
 #ifndef SW_DUO_SLACK
 #define SW_DUO_SLACK 0   // chunks a duo strip lets its producer lead by before it starts
 #endif
-template <int W, int C, bool M3, bool LIN>
+template <int W, int C, bool M3, bool LIN, bool RAW = false>
 __device__ void strip_pass_duo(const KParams& kp, const DuoDesc& d, const int strip, const int lane) {
     constexpr int SW = 64 * W;
     const int m = d.m_pad;
     const u16x2 go2 = splat2(kp.gap_init), ge2 = splat2(kp.gap_ext), ma2 = splat2(kp.match),
                 gom2 = splat2(kp.gap_init + kp.match);
-    StripDuo<W, M3, LIN> S;
+    StripDuo<W, M3, LIN, RAW> S;
     S.setup(kp, d, strip, lane);
     const bool has_in = strip > 0;
     const bool has_out = strip < d.strips - 1;
@@ -1043,7 +1081,7 @@ __device__ void strip_pass_duo(const KParams& kp, const DuoDesc& d, const int st
         raw1_nxt = fetch_raw(r1, k0 + C, lane, C, d.m[1]);
         if (has_in) await_granules<C>(kp, in_e, g, k0, lane, m, strip, failed);
         if (has_in) g_nxt = fetch_granules<C>(in_e, k0 + C, lane, m);
-        const unsigned code = codes_duo(raw0, raw1, k0, lane, C, d);
+        const unsigned code = codes_duo_t<RAW>(raw0, raw1, k0, lane, C, d);
         if (lane < C) {
             const bool real = has_in && k0 + lane < m;
             S.IOA = real ? g.y : as32(ma2);
@@ -1064,13 +1102,13 @@ __device__ void strip_pass_duo(const KParams& kp, const DuoDesc& d, const int st
 // and at 4 alike (tools/ubench_bank.hip).
 // M3: H = max3 and the running max fold two positions per v_pk_maximum3_f16
 // (scores below 0x7C00 only, LaunchCfg::duo_f16).
-template <int W, int C, bool M3, bool LIN>
+template <int W, int C, bool M3, bool LIN, bool RAW = false>
 __global__ void __launch_bounds__(64 * DUO_WAVES) sw_duo_kernel(KParams kp) {
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     for (int di = blockIdx.x; di < kp.npairs; di += gridDim.x) {
         const DuoDesc d = load_duo(kp, di);
-        for (int strip = wave; strip < d.strips; strip += DUO_WAVES) strip_pass_duo<W, C, M3, LIN>(kp, d, strip, lane);
+        for (int strip = wave; strip < d.strips; strip += DUO_WAVES) strip_pass_duo<W, C, M3, LIN, RAW>(kp, d, strip, lane);
     }
 }
 
@@ -1109,7 +1147,7 @@ struct DuoLink {
 // strip 0, wave 0) writes the table as it goes, two chunks ahead of its own reads and so of
 // every later strip's, after its first 128 rows (and the sentinels below row 0), then sets
 // *ready_out (the other waves wait for it before their first read of this duo's table).
-template <int W, int C, bool M3, bool LIN, bool TAB>
+template <int W, int C, bool M3, bool LIN, bool TAB, bool RAW = false>
 __device__ void strip_pass_duo_lds(const KParams& kp, const DuoDesc& d, const int strip, const int lane,
                                    const bool has_in, const DuoLink<LIN> in, const bool has_out,
                                    const DuoLink<LIN> out, int* const prod_out, int* const cons_out,
@@ -1133,7 +1171,7 @@ __device__ void strip_pass_duo_lds(const KParams& kp, const DuoDesc& d, const in
             for (int i = lane; i < DUO_TAB_OFF + 128; i += 64) {
                 const int row = i - DUO_TAB_OFF;
                 const unsigned q0 = fetch_raw(r0, row, 0, 1, d.m[0]), q1 = fetch_raw(r1, row, 0, 1, d.m[1]);
-                tab[i] = codes_duo(q0, q1, row, 0, 1, d);
+                tab[i] = codes_duo_t<RAW>(q0, q1, row, 0, 1, d);
             }
             raw0_nxt = fetch_raw(r0, 128, lane, C, d.m[0]);
             raw1_nxt = fetch_raw(r1, 128, lane, C, d.m[1]);
@@ -1144,7 +1182,7 @@ __device__ void strip_pass_duo_lds(const KParams& kp, const DuoDesc& d, const in
         raw0_nxt = fetch_raw(r0, 0, lane, C, d.m[0]);
         raw1_nxt = fetch_raw(r1, 0, lane, C, d.m[1]);
     }
-    std::conditional_t<TAB, StripDuoT<W, M3, LIN>, StripDuo<W, M3, LIN>> S;
+    std::conditional_t<TAB, StripDuoT<W, M3, LIN, RAW>, StripDuo<W, M3, LIN, RAW>> S;
     if constexpr (TAB) S.setup(kp, d, strip, lane, tab);
     else S.setup(kp, d, strip, lane);
     const long long t_start = (long long)__builtin_amdgcn_s_memrealtime();
@@ -1167,7 +1205,7 @@ __device__ void strip_pass_duo_lds(const KParams& kp, const DuoDesc& d, const in
         }
         if constexpr (TAB) {
             if (build) {   // table rows k0 + 128 .. k0 + 191 (bytes loaded a chunk ago), bytes of the next 64
-                tab[DUO_TAB_OFF + k0 + 128 + lane] = codes_duo(raw0, raw1, k0 + 128, lane, C, d);
+                tab[DUO_TAB_OFF + k0 + 128 + lane] = codes_duo_t<RAW>(raw0, raw1, k0 + 128, lane, C, d);
                 raw0_nxt = fetch_raw(r0, k0 + 192, lane, C, d.m[0]);
                 raw1_nxt = fetch_raw(r1, k0 + 192, lane, C, d.m[1]);
             }
@@ -1211,7 +1249,7 @@ __device__ void strip_pass_duo_lds(const KParams& kp, const DuoDesc& d, const in
         if constexpr (TAB) {
             S.template run<C>(k0, go2, ge2, ma2, gom2);
         } else {
-            S.IOR = codes_duo(raw0, raw1, k0, lane, C, d);
+            S.IOR = codes_duo_t<RAW>(raw0, raw1, k0, lane, C, d);
             S.template run<C>(go2, ge2, ma2, gom2);
         }
         if (has_out) {
@@ -1254,7 +1292,7 @@ __device__ void strip_pass_duo_lds(const KParams& kp, const DuoDesc& d, const in
 // after every wave has reported done with duo i - 1 (done[]), and the other waves read it
 // only after wave 0 has written its first rows (tabready).  Neither wait closes a cycle:
 // the waves finishing duo i - 1 need nothing from wave 0's duo i.
-template <int W, int C, bool M3, bool LIN, bool TAB>
+template <int W, int C, bool M3, bool LIN, bool TAB, bool RAW = false>
 __global__ void __launch_bounds__(64 * DUO_WAVES) sw_duo_lds_kernel(KParams kp) {
     static_assert(DUO_WAVES == 4, "the LDS links pair waves w -> w + 1 and 3 -> 0");
     using Slot = DuoSlot<LIN>;
@@ -1352,7 +1390,7 @@ __global__ void __launch_bounds__(64 * DUO_WAVES) sw_duo_lds_kernel(KParams kp) 
                                       wave > 0 ? base : 0, wave > 0 ? base : prev, &prod[(wave + 3) & 3], nullptr};
                 const DuoLink<LIN> out{wave < 3 ? ring[wave] : wrap, wave < 3 ? (unsigned)DUO_R - 1u : wmask,
                                        wave < 3 ? base : 0, base, nullptr, wave < 3 ? &cons[wave + 1] : nullptr};
-                strip_pass_duo_lds<W, C, M3, LIN, TAB>(kp, d, strip, lane, strip > 0, in, strip + 1 < d.strips, out,
+                strip_pass_duo_lds<W, C, M3, LIN, TAB, RAW>(kp, d, strip, lane, strip > 0, in, strip + 1 < d.strips, out,
                                                        prod_out, cons_out, sink[wave], tab, strip == 0, ready_out,
                                                        dseq + 1, prio_par, t_begin);
             }
@@ -1404,7 +1442,8 @@ hipError_t launch_t(const LaunchCfg& cfg, const KParams& kp, hipStream_t s) {
             }
             return hipErrorInvalidValue;
         case MODE_DUO:
-            if constexpr (DNA && C == 64) {
+            // byte batches (DNA false) run the same kernels with the penalty from the bytes (RAW)
+            if constexpr (C == 64) {
                 if (cfg.duo_wrap > 0) {   // every hand-off in LDS
                     const int dyn = duo_lds_dyn(cfg);
                     if (dyn > DUO_LDS_DYN_MAX) return hipErrorInvalidValue;
@@ -1417,27 +1456,26 @@ hipError_t launch_t(const LaunchCfg& cfg, const KParams& kp, hipStream_t s) {
                     };
                     if constexpr (W % 4 == 0) {
                         if (cfg.duo_tab > 0) {
-                            if (cfg.duo_f16 && cfg.f2_lin) return go(sw_duo_lds_kernel<W, C, true, true, true>);
-                            if (cfg.duo_f16) return go(sw_duo_lds_kernel<W, C, true, false, true>);
-                            return go(sw_duo_lds_kernel<W, C, false, false, true>);
+                            if (cfg.duo_f16 && cfg.f2_lin) return go(sw_duo_lds_kernel<W, C, true, true, true, !DNA>);
+                            if (cfg.duo_f16) return go(sw_duo_lds_kernel<W, C, true, false, true, !DNA>);
+                            return go(sw_duo_lds_kernel<W, C, false, false, true, !DNA>);
                         }
                     }
-                    if (cfg.duo_f16 && cfg.f2_lin) return go(sw_duo_lds_kernel<W, C, true, true, false>);
-                    if (cfg.duo_f16) return go(sw_duo_lds_kernel<W, C, true, false, false>);
-                    return go(sw_duo_lds_kernel<W, C, false, false, false>);
+                    if (cfg.duo_f16 && cfg.f2_lin) return go(sw_duo_lds_kernel<W, C, true, true, false, !DNA>);
+                    if (cfg.duo_f16) return go(sw_duo_lds_kernel<W, C, true, false, false, !DNA>);
+                    return go(sw_duo_lds_kernel<W, C, false, false, false, !DNA>);
                 }
             }
-            if constexpr (DNA) {
+            {
                 // the linear-gap step (G_INIT == G_EXT) is built with the f16-max3 form
                 if (cfg.duo_f16 && cfg.f2_lin)
-                    hipLaunchKernelGGL((sw_duo_kernel<W, C, true, true>), dim3(cfg.blocks), dim3(64 * DUO_WAVES), 0, s, kp);
+                    hipLaunchKernelGGL((sw_duo_kernel<W, C, true, true, !DNA>), dim3(cfg.blocks), dim3(64 * DUO_WAVES), 0, s, kp);
                 else if (cfg.duo_f16)
-                    hipLaunchKernelGGL((sw_duo_kernel<W, C, true, false>), dim3(cfg.blocks), dim3(64 * DUO_WAVES), 0, s, kp);
+                    hipLaunchKernelGGL((sw_duo_kernel<W, C, true, false, !DNA>), dim3(cfg.blocks), dim3(64 * DUO_WAVES), 0, s, kp);
                 else
-                    hipLaunchKernelGGL((sw_duo_kernel<W, C, false, false>), dim3(cfg.blocks), dim3(64 * DUO_WAVES), 0, s, kp);
+                    hipLaunchKernelGGL((sw_duo_kernel<W, C, false, false, !DNA>), dim3(cfg.blocks), dim3(64 * DUO_WAVES), 0, s, kp);
                 break;
             }
-            return hipErrorInvalidValue;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
@@ -1446,18 +1484,18 @@ hipError_t launch_t(const LaunchCfg& cfg, const KParams& kp, hipStream_t s) {
 template <int W, int C, bool DNA>
 int waves_t(const LaunchCfg& cfg) {
     const int mode = cfg.mode;
-    if constexpr (DNA && C == 64) {
+    if constexpr (C == 64) {
         if (mode == MODE_DUO && cfg.duo_wrap > 0) {
             const int dyn = duo_lds_dyn(cfg);
             if constexpr (W % 4 == 0) {
                 if (cfg.duo_tab > 0)
-                    return cfg.f2_lin    ? occupancy_waves(sw_duo_lds_kernel<W, C, true, true, true>, 64 * DUO_WAVES, dyn)
-                           : cfg.duo_f16 ? occupancy_waves(sw_duo_lds_kernel<W, C, true, false, true>, 64 * DUO_WAVES, dyn)
-                                         : occupancy_waves(sw_duo_lds_kernel<W, C, false, false, true>, 64 * DUO_WAVES, dyn);
+                    return cfg.f2_lin    ? occupancy_waves(sw_duo_lds_kernel<W, C, true, true, true, !DNA>, 64 * DUO_WAVES, dyn)
+                           : cfg.duo_f16 ? occupancy_waves(sw_duo_lds_kernel<W, C, true, false, true, !DNA>, 64 * DUO_WAVES, dyn)
+                                         : occupancy_waves(sw_duo_lds_kernel<W, C, false, false, true, !DNA>, 64 * DUO_WAVES, dyn);
             }
-            return cfg.f2_lin    ? occupancy_waves(sw_duo_lds_kernel<W, C, true, true, false>, 64 * DUO_WAVES, dyn)
-                   : cfg.duo_f16 ? occupancy_waves(sw_duo_lds_kernel<W, C, true, false, false>, 64 * DUO_WAVES, dyn)
-                                 : occupancy_waves(sw_duo_lds_kernel<W, C, false, false, false>, 64 * DUO_WAVES, dyn);
+            return cfg.f2_lin    ? occupancy_waves(sw_duo_lds_kernel<W, C, true, true, false, !DNA>, 64 * DUO_WAVES, dyn)
+                   : cfg.duo_f16 ? occupancy_waves(sw_duo_lds_kernel<W, C, true, false, false, !DNA>, 64 * DUO_WAVES, dyn)
+                                 : occupancy_waves(sw_duo_lds_kernel<W, C, false, false, false, !DNA>, 64 * DUO_WAVES, dyn);
         }
     }
     switch (mode) {
@@ -1468,8 +1506,7 @@ int waves_t(const LaunchCfg& cfg) {
             if constexpr (DNA) return occupancy_waves(sw_flow_kernel<W, C>);
             return 0;
         case MODE_DUO:
-            if constexpr (DNA) return occupancy_waves(sw_duo_kernel<W, C, true, false>, 64 * DUO_WAVES);
-            return 4;
+            return occupancy_waves(sw_duo_kernel<W, C, true, false, !DNA>, 64 * DUO_WAVES);
         default: return 4;
     }
 }

@@ -182,7 +182,8 @@ void sw_db_close(sw_db* db);
  *   "orient"   0 = auto, 1 = seq1 spread across lanes, 2 = seq2 across lanes
  *   "mode"     -1 = auto, 0 = independent strip waves, 1 = workgroup per pair,
  *              2 = lock-step strip groups (single long pairs),
- *              3 = packed 16-bit pair duos (DNA batches with scores < 65535),
+ *              3 = packed 16-bit pair duos (batches with scores < 65535: DNA, and any bytes
+ *                  when MISMATCH < 0 and MATCH - MISMATCH <= 127, option duo_raw),
  *              4 = free-running strip groups, rows staged in LDS (long DNA pairs),
  *              5 = the flow2 / flow3 wavefront step (DNA, one column per lane or more, chunked
  *                  LDS / granule hand-offs; the automatic plan for single long pairs, column
@@ -228,6 +229,10 @@ void sw_db_close(sw_db* db);
  *              columns per lane, when the table and the wrap buffer fit two workgroups per CU
  *              and the duos run in one pass at that), 2 = whenever it fits, 0 = the codes travel
  *              lane to lane by DPP
+ *   "duo_raw"  1 = (default) byte batches (any byte outside {A,C,G,T}: protein, N, lower case) run the
+ *              duo kernels with the penalty from the bytes (one XOR and one v_pk_min_u16 per position
+ *              for the DNA step's v_perm_b32; needs MISMATCH < 0, MATCH - MISMATCH <= 127), 0 = the
+ *              byte-path strip kernels
  *   "duo_prio" -1 = (default) auto: 17 for the duo LDS kernel with the row-code table, else 0;
  *              k in 6..20: a CU's two duo workgroups take turns at issue priority (s_setprio) in
  *              slices of 2^k ticks (10 ns) of the clock from their start; 0 = off (timing only)
