@@ -283,6 +283,9 @@ def kernel_label(st):
                 ("sw_flow3ra3p_kernel" if aff3 else "sw_flow3r3p_kernel") if v & 32768 else \
                 ("sw_flow3r" if ring else "sw_flow3") + ("a" if aff3 else "") + ("3" if v & 8192 else "") + \
                 ("s" if v & 2048 else "") + "_kernel"
+            if v & 65536:   # a pair over up to seven byte values (sw_flow3h / sw_flow3ah_kernel)
+                name += ", seven-letter alphabet"
+                fn = "sw_flow3ah_kernel" if aff3 else "sw_flow3h_kernel"
             if v & 2048:
                 name += ", column slab (peer edges)"
         else:
@@ -295,6 +298,8 @@ def kernel_label(st):
         name = "duo" + (" LDS hand-offs" if v & 128 else " granules") + (", row-code table" if v & 256 else "") + \
                (", f16-max3" if v & 1 else "")
         fn = "sw_duo_lds_kernel" if v & 128 else "sw_duo_kernel"
+        if st.get("dna") == 0:
+            name += ", raw bytes"
         lin = bool(v & 8)
     else:
         name = {0: "strip", 1: "pairwg", 2: "chain", 4: "flow"}.get(mode, str(mode))

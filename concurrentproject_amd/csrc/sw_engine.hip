@@ -66,7 +66,7 @@ std::atomic<long long> g_opt_W{0}, g_opt_C{0}, g_opt_bytes{0}, g_opt_timeout{30}
     g_opt_mode{-1}, g_opt_trace{0}, g_opt_duo_f16{1}, g_opt_f2stream{0}, g_opt_ring{-1}, g_opt_ring_rows{4096}, g_opt_f2_wgs{0}, g_opt_f2w{0}, g_opt_f2pwg{-1},
     g_opt_linear{-1}, g_opt_f3{1}, g_opt_slab_plain{0}, g_opt_duo_lds{1}, g_opt_duo_tab{1}, g_opt_duo_roles{1}, g_opt_f3hl{1},
     g_opt_f3rhl{0}, g_opt_f3a{1}, g_opt_f3slab{1}, g_opt_duo_prio{-1}, g_opt_f3pool{0},
-    g_opt_stall_item{-1}, g_opt_f3pwg{1}, g_opt_duo_raw{1};
+    g_opt_stall_item{-1}, g_opt_f3pwg{1}, g_opt_duo_raw{1}, g_opt_hep{1};
 
 // Longest sequence the engine takes: granule buffers of m rows keep m * 16 in the
 // 32-bit record count of a buffer resource (sw_device.h linear_edge).
@@ -207,6 +207,9 @@ struct Job {
     int w45_s4 = -1;             // with f2w3: four / five columns per lane instead (sw_flow3r45_kernel, plan_w45)
     bool f3pwg = false;          // with pwg: flow3's three-column ring step, a pair per workgroup (plan_pwg3)
     bool pwg = false;            // MODE_FLOW2 batch: a pair per workgroup (sw_flow2.hip PWG)
+    int hep = 0;                 // one pair over 1..7 byte values not all in {A,C,G,T}: their count (planned as
+                                 // DNA, run on flow3's staged kernels, sw_flow3.hip HEP); 0 otherwise
+    unsigned char hsym[256] = {};   // with hep: each byte value's symbol 0..6
 };
 
 bool is_dna_byte(unsigned char c) { return c == 'A' || c == 'C' || c == 'G' || c == 'T'; }
@@ -493,6 +496,56 @@ void plan_claim(Job& job, const Params& prm) {
     job.C = 64;
     plan_flow2(job, flow2_w2_wanted(job, prm));
     job.f2_stream = true;
+}
+
+// A pair's byte set (256 bits) -> job.hep / job.hsym: at most seven values, not all within {A,C,G,T}
+// (those take the DNA path), symbols in byte order.  Option hep = 0: never.
+bool set_hep(Job& job, const uint32_t set[8]) {
+    job.hep = 0;
+    if (g_opt_hep.load() == 0) return false;
+    int k = 0;
+    unsigned char sym[256] = {};
+    for (int b = 0; b < 256; ++b)
+        if (set[b >> 5] >> (b & 31) & 1u) {
+            if (k == 7) return false;
+            sym[b] = (unsigned char)k++;
+        }
+    if (k == 0) return false;
+    std::memcpy(job.hsym, sym, sizeof sym);
+    job.hep = k;
+    return true;
+}
+
+void byte_set(const unsigned char* p, int len, uint32_t set[8]) {
+    for (int i = 0; i < len; ++i) set[p[i] >> 5] |= 1u << (p[i] & 31);
+}
+
+// The staged flow3 launch enqueue would make of a planned single-pair job (use_f3 without ring or
+// streamed rows, or use_f3a): the only kernels with seven-letter alphabets (HEP)
+bool hep_staged(const Job& job, const Params& prm) {
+    if (job.mode != MODE_FLOW2 || job.ring || job.f2_stream || job.slab || job.pwg || job.f3pwg ||
+        g_opt_f3pool.load() != 0 || job.pairs.size() != 1)
+        return false;
+    const int max_m = job.pairs[0].m;
+    const bool lin = prm.gap_init == prm.gap_ext && g_opt_linear.load() != 0 &&
+                     (job.C == 32 || job.C == 64 || (job.C == 16 && job.f2w2));
+    if (job.f2w2) return lin && g_opt_f3.load() != 0 && flow3_fits(max_m, job.C);
+    return !lin && g_opt_f3a.load() != 0 && (job.C == 32 || job.C == 16) && flow3_fits(max_m, job.C, true);
+}
+
+int finalize_mode(Job& job, const Params& prm, int cus);
+
+// finalize_mode, and for a seven-letter job (planned as DNA) the check that it lands on the staged flow3
+// kernels; otherwise the job is re-planned on the byte path
+int finalize_alphabet(Job& job, const Params& prm, int cus, bool single) {
+    if (job.hep) job.dna = true;
+    if (finalize_mode(job, prm, cus)) return -1;
+    if (!job.hep || hep_staged(job, prm)) return 0;
+    job.hep = 0;
+    job.dna = false;
+    const int W = pick_W(job.pairs, single);
+    plan(job, W, pick_C(W), single);
+    return finalize_mode(job, prm, cus);
 }
 
 int finalize_mode(Job& job, const Params& prm, int cus) {
@@ -938,6 +991,11 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
     cfg.f3p = g_opt_f3pool.load() != 0 && cfg.f3_hl && job.C == 32 && !job.ring && (use_f3 || use_f3a);
     cfg.f3_w3 = job.f2w3 && job.w45_s4 < 0;
     cfg.f3_w45 = job.w45_s4 >= 0;
+    cfg.hep = job.hep > 0;
+    if (cfg.hep && !((use_f3 && !f2s && !job.ring) || use_f3a) ) {
+        set_err("a seven-letter alphabet runs flow3's staged kernels only (one pair, rows in LDS)");
+        return -1;
+    }
     cfg.f3_pwg = job.f3pwg;
     if (job.f3pwg) {   // the linear-gap ring step, or the affine one (sw_flow3ra3p_kernel)
         cfg.f3 = f2_lin;
@@ -1011,6 +1069,27 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
         for (int r = 0; r < 4; ++r) w |= (unsigned)((r == q ? prm.match : prm.mismatch) & 0xFF) << (8 * r);
         kp.prof3[q] = w;
     }
+    if (cfg.hep) {   // seven-letter alphabet: per column symbol c, row symbols 0..3 high, 4..6 low (sw_flow3.hip HEP)
+        std::memcpy(kp.hsym, job.hsym, sizeof kp.hsym);
+        for (int c = 0; c < 7; ++c) {
+            unsigned p2 = 0, q2 = 0x80u, p3 = 0, q3 = 0x80u;
+            for (int r = 0; r < 7; ++r) {
+                const int sc = r == c ? prm.match : prm.mismatch;
+                const unsigned b2 = (unsigned)((sc + prm.gap_init) & 0xFF), b3 = (unsigned)(sc & 0xFF);
+                if (r < 4) {
+                    p2 |= b2 << (8 * r);
+                    p3 |= b3 << (8 * r);
+                } else {
+                    q2 |= b2 << (8 * (r - 3));
+                    q3 |= b3 << (8 * (r - 3));
+                }
+            }
+            kp.hp2[c] = p2;
+            kp.hq2[c] = q2;
+            kp.hp3[c] = p3;
+            kp.hq3[c] = q3;
+        }
+    }
     for (int q = 0; q < 4; ++q) {   // duo: penalty bytes MATCH - s(r, q)
         unsigned w = 0;
         for (int r = 0; r < 4; ++r) w |= (unsigned)(r == q ? 0 : prm.match - prm.mismatch) << (8 * r);
@@ -1052,7 +1131,7 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
     t_stats.cells = job.cells;
     t_stats.W = job.W;
     t_stats.C = job.C;
-    t_stats.dna = job.dna ? 1 : 0;
+    t_stats.dna = job.hep ? 2 : job.dna ? 1 : 0;   // 2: a seven-letter alphabet on the DNA kernels
     t_stats.blocks = cfg.blocks;
     t_stats.waves_per_cu = wpc;
     t_stats.items = items;
@@ -1061,7 +1140,7 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
                       (cfg.f2_w2 ? 16 : 0) | (cfg.f2_pwg ? 32 : 0) | (cfg.f3 ? 64 : 0) | (cfg.duo_wrap > 0 ? 128 : 0) |
                       (cfg.duo_tab > 0 ? 256 : 0) | (cfg.f3_hl ? 512 : 0) | (cfg.f3a || cfg.f3ra ? 1024 : 0) |
                       (cfg.f3_slab ? 2048 : 0) | (cfg.f3p ? 4096 : 0) | (cfg.f3_w3 ? 8192 : 0) |
-                      (cfg.f3_w45 ? 16384 : 0) | (cfg.f3_pwg ? 32768 : 0);
+                      (cfg.f3_w45 ? 16384 : 0) | (cfg.f3_pwg ? 32768 : 0) | (cfg.hep ? 65536 : 0);
     t_stats.boundary_bytes = (long long)(job.bnd_granules * sizeof(Granule));
     c->last = s;
     return 0;
@@ -1151,9 +1230,15 @@ int launch_host(Ctx* c, const HostPair* in, const std::vector<int>& act, const P
         d.m = m;
         d.out_idx = full ? act[i] : (int)i;
     }
+    if (!dna && single && g_opt_bytes.load() == 0) {
+        uint32_t set[8] = {};
+        byte_set(in[act[0]].s1, in[act[0]].n, set);
+        byte_set(in[act[0]].s2, in[act[0]].m, set);
+        set_hep(job, set);
+    }
     const int W = pick_W(job.pairs, single);
     plan(job, W, pick_C(W), single);
-    if (finalize_mode(job, prm, c->cus)) return -1;
+    if (finalize_alphabet(job, prm, c->cus, single)) return -1;
     if (c->seq.ensure(bytes, s)) return -1;
     HIPCHK(hipMemcpyAsync(c->seq.p, c->hseq.p, bytes, hipMemcpyHostToDevice, s));
     return enqueue(c, job, prm, c->seq.p, d_scores, nscores, s, true);
@@ -1223,20 +1308,25 @@ int score_one(const unsigned char* s1, const unsigned char* s2, int n, int m, co
     return sc;
 }
 
-__global__ void alphabet_kernel(const unsigned char* arena, const PairDesc* pairs, int npairs, unsigned* flag) {
+// flag[0] |= 1 when a byte outside {A,C,G,T} occurs; with set (one pair): flag[1..8] |= the byte set
+__global__ void alphabet_kernel(const unsigned char* arena, const PairDesc* pairs, int npairs, unsigned* flag, int set) {
+    __shared__ unsigned bits[8];
     const int k = blockIdx.x;
     if (k >= npairs) return;
+    if (threadIdx.x < 8) bits[threadIdx.x] = 0u;
+    __syncthreads();
     const PairDesc d = pairs[k];
     unsigned bad = 0;
-    for (int i = threadIdx.x; i < d.n; i += blockDim.x) {
-        const unsigned char ch = arena[d.col_off + i];
-        bad |= !(ch == 'A' || ch == 'C' || ch == 'G' || ch == 'T');
-    }
-    for (int i = threadIdx.x; i < d.m; i += blockDim.x) {
-        const unsigned char ch = arena[d.row_off + i];
-        bad |= !(ch == 'A' || ch == 'C' || ch == 'G' || ch == 'T');
+    for (int i = threadIdx.x; i < d.n + d.m; i += blockDim.x) {
+        const unsigned char ch = i < d.n ? arena[d.col_off + i] : arena[d.row_off + (i - d.n)];
+        const bool b = !(ch == 'A' || ch == 'C' || ch == 'G' || ch == 'T');
+        bad |= b;
+        // (a read before the atomic: only a value's first sightings write)
+        if (set && !(bits[ch >> 5] >> (ch & 31) & 1u)) atomicOr(&bits[ch >> 5], 1u << (ch & 31));
     }
     if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(flag, 1u);
+    __syncthreads();
+    if (set && threadIdx.x < 8 && bits[threadIdx.x]) atomicOr(flag + 1 + threadIdx.x, bits[threadIdx.x]);
 }
 
 }  // namespace
@@ -1660,18 +1750,26 @@ int sw_score_batch_device(const unsigned char* d_arena, const int64_t* a_off, co
             HIPCHK(hipEventSynchronize(c->staged));
             c->staged_pending = false;
         }
-        if (c->hdesc.ensure(np) || c->desc.ensure(np, s) || c->flag.ensure(1, s) || c->hctrl.ensure(1)) return -1;
+        // (one pair: the byte set too, for the seven-letter path)
+        const int set = single && g_opt_hep.load() != 0 ? 1 : 0;
+        // (the pinned control block, 3 x 16 B, takes the flag and the byte set back)
+        if (c->hdesc.ensure(np) || c->desc.ensure(np, s) || c->flag.ensure(9, s) || c->hctrl.ensure(3)) return -1;
         std::memcpy(c->hdesc.p, job.pairs.data(), np * sizeof(PairDesc));
         HIPCHK(hipMemcpyAsync(c->desc.p, c->hdesc.p, np * sizeof(PairDesc), hipMemcpyHostToDevice, s));
-        HIPCHK(hipMemsetAsync(c->flag.p, 0, sizeof(unsigned), s));
-        hipLaunchKernelGGL(alphabet_kernel, dim3((unsigned)np), dim3(256), 0, s, d_arena, c->desc.p, (int)np, c->flag.p);
+        HIPCHK(hipMemsetAsync(c->flag.p, 0, 9 * sizeof(unsigned), s));
+        hipLaunchKernelGGL(alphabet_kernel, dim3((unsigned)np), dim3(256), 0, s, d_arena, c->desc.p, (int)np, c->flag.p, set);
         HIPCHK(hipGetLastError());
         unsigned* hflag = reinterpret_cast<unsigned*>(c->hctrl.p);
-        HIPCHK(hipMemcpyAsync(hflag, c->flag.p, sizeof(unsigned), hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(hflag, c->flag.p, 9 * sizeof(unsigned), hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
-        job.dna = *hflag == 0;
+        job.dna = hflag[0] == 0;
+        if (!job.dna && set) {
+            uint32_t bits[8];
+            std::memcpy(bits, hflag + 1, sizeof bits);
+            set_hep(job, bits);
+        }
     }
-    if (finalize_mode(job, prm, c->cus)) return -1;
+    if (finalize_alphabet(job, prm, c->cus, single)) return -1;
     if (enqueue(c, job, prm, d_arena, d_scores, npairs, s, !stream)) return -1;
     if (!stream) {
         if (check_ctrl(c, s)) return -1;
@@ -1851,6 +1949,9 @@ int sw_set_option(const char* key, long long v) {
     } else if (k == "f3pwg") {   // 1 (default): int32 batches on flow3's three-column ring step, a pair per
         // workgroup (sw_flow3r3p_kernel, affine: sw_flow3ra3p_kernel); 0: flow2's pair-per-workgroup kernel
         g_opt_f3pwg = v ? 1 : 0;
+    } else if (k == "hep") {   // 1 (default): one pair over up to seven byte values on flow3's staged kernels, 0: byte path
+        if (v < 0 || v > 1) return -1;
+        g_opt_hep = v;
     } else if (k == "duo_raw") {   // 1 (default): byte batches on the duo kernels (RAW penalty), 0: byte strip kernels
         if (v < 0 || v > 1) return -1;
         g_opt_duo_raw = v;
@@ -1943,6 +2044,7 @@ long long sw_get_option(const char* key) {
     if (k == "stall_item") return g_opt_stall_item;
     if (k == "f3pwg") return g_opt_f3pwg;
     if (k == "duo_raw") return g_opt_duo_raw;
+    if (k == "hep") return g_opt_hep;
     if (k == "blocks") return g_opt_blocks;
     if (k == "orient") return g_opt_orient;
     if (k == "trace") return g_opt_trace;

@@ -77,6 +77,12 @@ struct KParams {
     unsigned prof2[4];            // flow2 mode: per column code, 4 signed score bytes s + G_INIT (row code 0..3)
     unsigned prof3[4];            // flow2 W2: per column code, 4 signed score bytes s (row code 0..3)
     unsigned pen[4];              // duo mode: per column code, 4 penalty bytes MATCH - s (row code 0..3)
+    // a pair over an alphabet of up to seven byte values (flow3 staged, LaunchCfg::hep): the symbol
+    // 0..6 of each byte value, and per column symbol the perm's high word (row symbols 0..3) and low
+    // word (byte 0: the no-row 0x80; bytes 1..3: row symbols 4..6), as signed bytes s + G_INIT (hp2,
+    // hq2) and s (hp3, hq3)
+    unsigned char hsym[256];
+    unsigned hp2[7], hq2[7], hp3[7], hq3[7];
     const DuoDesc* duos;          // duo mode: nduos descriptors (npairs counts duos)
     long long timeout_ticks;      // s_memrealtime ticks (100 MHz) before a spin gives up
     unsigned long long* trace;    // optional (tools/trace_flow.py): per-strip timestamps, else null
@@ -143,6 +149,7 @@ struct LaunchCfg {
     bool f3_hl = false;     // flow3 staged at C = 32: in-workgroup links hand off every half chunk
     bool f3a = false;       // MODE_FLOW2 staged one-column launch with the affine step on flow3 (sw_flow3a_kernel)
     bool f3p = false;       // flow3 staged on the pool loops (sw_flow3p_kernel: C = 32, f3_hl, no I/O rotation)
+    bool hep = false;       // flow3 staged launch of a pair over up to seven byte values (sw_flow3h / ah_kernel, KParams::hsym)
     bool f3_w3 = false;     // flow3 ring mode at three columns per lane (sw_flow3r3_kernel / sw_flow3r3s_kernel)
     bool f3_w45 = false;    // flow3 ring mode at four and five columns per lane (sw_flow3r45_kernel, KParams::w45_s4)
     bool f3_pwg = false;    // flow3 three-column ring step, a pair per workgroup (sw_flow3r3p_kernel; int32 batches)

@@ -229,6 +229,9 @@ void sw_db_close(sw_db* db);
  *              columns per lane, when the table and the wrap buffer fit two workgroups per CU
  *              and the duos run in one pass at that), 2 = whenever it fits, 0 = the codes travel
  *              lane to lane by DPP
+ *   "hep"      1 = (default) one pair over at most seven byte values not all in {A,C,G,T} (ACGTN,
+ *              lower case, RNA) runs flow3's staged kernels with 3-bit row symbols (sw_flow3h /
+ *              sw_flow3ah_kernel; rows that fit in LDS, else the byte path), 0 = the byte path
  *   "duo_raw"  1 = (default) byte batches (any byte outside {A,C,G,T}: protein, N, lower case) run the
  *              duo kernels with the penalty from the bytes (one XOR and one v_pk_min_u16 per position
  *              for the DNA step's v_perm_b32; needs MISMATCH < 0, MATCH - MISMATCH <= 127), 0 = the
@@ -266,7 +269,9 @@ typedef struct {
                                bit 13: flow3 ring at three columns per lane (sw_flow3r3 / ra3 kernels);
                                bit 14: flow3 ring at four / five columns per lane (sw_flow3r45_kernel);
                                bit 15: flow3 three-column ring step with a pair per workgroup
-                                       (sw_flow3r3p_kernel / sw_flow3ra3p_kernel: int32 batches) */
+                                       (sw_flow3r3p_kernel / sw_flow3ra3p_kernel: int32 batches);
+                               bit 16: a pair over up to seven byte values on flow3's staged kernels
+                                       (option hep; dna = 2 then) */
 } sw_stats;
 int sw_last_stats(sw_stats* out);
 

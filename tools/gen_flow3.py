@@ -283,8 +283,10 @@ def gen_role(IN, OUT_, spec=0, halfpub=True, C=32, hl=False):
                     a(f"L_midr{p}_%=:")
                     a(f"s_waitcnt lgkmcnt({2 if lds_out else 0})")
                     a("v_cndmask_b32_e64 v64, v64, v102, s[50:51]")
-            a(f"v_perm_b32 v72, %[pA], %[k80], v{cur + u}")
-            a(f"v_perm_b32 v73, %[pB], %[k80], v{cur + u}")
+            # score bytes of 4 rows: selectors 4..7 pick pA (row symbols 0..3), 0..3 pick qA (0: no row,
+            # 0x80; 1..3: row symbols 4..6 of a seven-letter alphabet, sw_flow3.hip HEP; DNA: 0x80808080)
+            a(f"v_perm_b32 v72, %[pA], %[qA], v{cur + u}")
+            a(f"v_perm_b32 v73, %[pB], %[qB], v{cur + u}")
             for b in range(4):
                 io, l0 = ("v64", "v65") if b % 2 == 0 else ("v65", "v64")
                 step(a, io, l0, b)
@@ -383,8 +385,8 @@ def emit(spec=0, halfpub=True):
                 for line in body:
                     out.append('        "%s\\n\\t"' % line)
                 out.append('        : [M] "=v"(r.M), [fail] "=s"(r.fail), [slow] "=s"(r.slow)')
-                out.append('        : [pA] "v"(x.pA), [pB] "v"(x.pB), [ng] "v"(x.ng), [G] "s"(x.G), [k80] "s"(x.k80),')
-                out.append('          [code] "v"(x.code), [lin] "v"(x.lin), [lout] "v"(x.lout), [pin] "v"(x.pin),')
+                out.append('        : [pA] "v"(x.pA), [pB] "v"(x.pB), [ng] "v"(x.ng), [G] "s"(x.G), [qA] "v"(x.qA),')
+                out.append('          [qB] "v"(x.qB), [code] "v"(x.code), [lin] "v"(x.lin), [lout] "v"(x.lout), [pin] "v"(x.pin),')
                 out.append('          [pout] "v"(x.pout), [qme] "v"(x.qme), [qnx] "v"(x.qnx), [end] "s"(x.end),')
                 out.append('          [dlo] "s"(x.dlo), [dhi] "s"(x.dhi), [rsrc] "s"(x.rsrc), [ek] "s"(x.ek),')
                 out.append('          [lrow] "v"(x.lrow), [m48] "s"(x.m48), [lmid] "v"(x.lmid)')
@@ -1145,7 +1147,7 @@ def gen_role_aff(IN, OUT_, C=32, hl=True):
                     a(f"s_waitcnt lgkmcnt({2 if lds_out else 0})")
                     a("v_cndmask_b32_e64 v64, v64, v106, s[50:51]")
                     a("v_cndmask_b32_e64 v65, v65, v107, s[50:51]")
-            a(f"v_perm_b32 v75, %[pA], %[k80], v{cur + u}")
+            a(f"v_perm_b32 v75, %[pA], %[qA], v{cur + u}")
             for b in range(4):
                 step_aff1(a, b, b % 2 == 0)
             if gran and u == ng // 2 - 1:
@@ -1202,7 +1204,7 @@ def emit_aff():
                     out.append('        "%s\\n\\t"' % line)
                 out.append('        : [M] "=v"(r.M), [fail] "=s"(r.fail), [slow] "=s"(r.slow)')
                 out.append('        : [pA] "v"(x.pA), [ng] "v"(x.ng), [nge] "v"(x.nge), [GI] "s"(x.GI), [GE] "s"(x.GE),')
-                out.append('          [k80] "s"(x.k80), [code] "v"(x.code), [lin] "v"(x.lin), [lout] "v"(x.lout),')
+                out.append('          [qA] "v"(x.qA), [code] "v"(x.code), [lin] "v"(x.lin), [lout] "v"(x.lout),')
                 out.append('          [pin] "v"(x.pin), [pout] "v"(x.pout), [qme] "v"(x.qme), [qnx] "v"(x.qnx),')
                 out.append('          [end] "s"(x.end), [dlo] "s"(x.dlo), [dhi] "s"(x.dhi), [rsrc] "s"(x.rsrc),')
                 out.append('          [ek] "s"(x.ek), [ek2] "s"(x.ek2), [lrow] "v"(x.lrow), [m48] "s"(x.m48),')
