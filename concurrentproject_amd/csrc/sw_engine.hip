@@ -145,6 +145,7 @@ struct Ctx {
     DevBuf<int> scores;
     DevBuf<unsigned> flag;
     DevBuf<unsigned> cons;            // flow2 ring mode: consumer progress words
+    DevBuf<unsigned char> hrows;      // a seven-letter ring launch: the pair's rows as perm selectors
     DevBuf<DuoDesc> duo;
     PinBuf<DuoDesc> hduo;
     PinBuf<unsigned char> hseq;
@@ -520,15 +521,18 @@ void byte_set(const unsigned char* p, int len, uint32_t set[8]) {
     for (int i = 0; i < len; ++i) set[p[i] >> 5] |= 1u << (p[i] & 31);
 }
 
-// The staged flow3 launch enqueue would make of a planned single-pair job (use_f3 without ring or
-// streamed rows, or use_f3a): the only kernels with seven-letter alphabets (HEP)
-bool hep_staged(const Job& job, const Params& prm) {
-    if (job.mode != MODE_FLOW2 || job.ring || job.f2_stream || job.slab || job.pwg || job.f3pwg ||
-        g_opt_f3pool.load() != 0 || job.pairs.size() != 1)
-        return false;
+// The flow3 launch enqueue would make of a planned single-pair job, when it is one of the kernels with
+// seven-letter alphabets (HEP): staged (use_f3 without ring or streamed rows, or use_f3a), or ring mode at
+// three columns per lane, whole-chunk links (sw_flow3r3h / ra3h_kernel)
+bool hep_launchable(const Job& job, const Params& prm) {
+    if (job.mode != MODE_FLOW2 || job.slab || job.pwg || job.f3pwg || job.pairs.size() != 1) return false;
     const int max_m = job.pairs[0].m;
     const bool lin = prm.gap_init == prm.gap_ext && g_opt_linear.load() != 0 &&
                      (job.C == 32 || job.C == 64 || (job.C == 16 && job.f2w2));
+    if (job.ring)
+        return job.f2w2 && job.f2w3 && job.w45_s4 < 0 && job.C == 64 && g_opt_f3rhl.load() == 0 &&
+               g_opt_f3slab.load() != 0 && (lin ? g_opt_f3.load() != 0 : g_opt_f3a.load() != 0);
+    if (job.f2_stream || g_opt_f3pool.load() != 0) return false;
     if (job.f2w2) return lin && g_opt_f3.load() != 0 && flow3_fits(max_m, job.C);
     return !lin && g_opt_f3a.load() != 0 && (job.C == 32 || job.C == 16) && flow3_fits(max_m, job.C, true);
 }
@@ -540,7 +544,7 @@ int finalize_mode(Job& job, const Params& prm, int cus);
 int finalize_alphabet(Job& job, const Params& prm, int cus, bool single) {
     if (job.hep) job.dna = true;
     if (finalize_mode(job, prm, cus)) return -1;
-    if (!job.hep || hep_staged(job, prm)) return 0;
+    if (!job.hep || hep_launchable(job, prm)) return 0;
     job.hep = 0;
     job.dna = false;
     const int W = pick_W(job.pairs, single);
@@ -773,6 +777,15 @@ struct SlabEdge {
     unsigned epoch;
 };
 
+// A seven-letter ring launch's rows as perm selectors (sw_flow3.hip HEP: 4 + s for symbols 0..3,
+// s - 3 for 4..6), streamed by the ring loops as they are
+struct HepSel {
+    unsigned char sel[256];
+};
+__global__ void hep_rows_kernel(const unsigned char* rows, int m, unsigned char* out, HepSel t) {
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < m; i += gridDim.x * blockDim.x) out[i] = t.sel[rows[i]];
+}
+
 // Enqueue the launch for a planned job whose sequences are in `d_seq`.
 int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int* d_scores, int nscores,
             hipStream_t s, bool time_kernel, const SlabEdge* edge = nullptr) {
@@ -895,6 +908,7 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
         probe.f3_w45 = use_f3 && job.w45_s4 >= 0;
         probe.f3_slab = (use_f3 || use_f3ra) && edge != nullptr;
         if (probe.f3_slab) probe.f3_hl = false;
+        probe.hep = job.hep > 0;
         int fit = 0;
         for (;; --f2_wgs) {
             probe.f2_wgs = f2_wgs;
@@ -992,8 +1006,9 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
     cfg.f3_w3 = job.f2w3 && job.w45_s4 < 0;
     cfg.f3_w45 = job.w45_s4 >= 0;
     cfg.hep = job.hep > 0;
-    if (cfg.hep && !((use_f3 && !f2s && !job.ring) || use_f3a) ) {
-        set_err("a seven-letter alphabet runs flow3's staged kernels only (one pair, rows in LDS)");
+    if (cfg.hep && !((use_f3 && !f2s && !job.ring) || use_f3a ||
+                     ((use_f3 || use_f3ra) && job.ring && cfg.f3_w3 && edge == nullptr && !job.f3pwg))) {
+        set_err("a seven-letter alphabet runs flow3's staged kernels or its three-column ring kernels only (one pair)");
         return -1;
     }
     cfg.f3_pwg = job.f3pwg;
@@ -1122,6 +1137,19 @@ int enqueue(Ctx* c, Job& job, const Params& prm, const unsigned char* d_seq, int
         kp.slab_epoch = edge->epoch;
     }
 
+    if (cfg.hep && job.ring) {   // the rows as selectors, once per launch (m bytes, before the timed kernel)
+        const PairDesc& d = job.pairs[0];
+        if (c->hrows.ensure((size_t)d.m, s)) return -1;
+        HepSel t{};
+        for (int b = 0; b < 256; ++b) {
+            const unsigned sym = job.hsym[b];
+            t.sel[b] = (unsigned char)(sym < 4 ? 4 + sym : sym - 3);
+        }
+        hipLaunchKernelGGL(hep_rows_kernel, dim3((unsigned)std::min(1024, (d.m + 255) / 256)), dim3(256), 0, s,
+                           d_seq + d.row_off, d.m, c->hrows.p, t);
+        HIPCHK(hipGetLastError());
+        kp.hrows = c->hrows.p;
+    }
     if (time_kernel) HIPCHK(hipEventRecord(c->ev0, s));
     HIPCHK(cfg.f3 || cfg.f3a || cfg.f3ra ? launch_sw_flow3(cfg, kp, s)
            : job.mode == MODE_FLOW2 ? launch_sw_flow2(cfg, kp, s) : launch_sw_strip(cfg, kp, s));

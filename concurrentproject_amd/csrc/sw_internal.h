@@ -83,6 +83,7 @@ struct KParams {
     // hq2) and s (hp3, hq3)
     unsigned char hsym[256];
     unsigned hp2[7], hq2[7], hp3[7], hq3[7];
+    const unsigned char* hrows;   // ring mode (sw_flow3r3h / ra3h_kernel): the pair's rows as perm selectors
     const DuoDesc* duos;          // duo mode: nduos descriptors (npairs counts duos)
     long long timeout_ticks;      // s_memrealtime ticks (100 MHz) before a spin gives up
     unsigned long long* trace;    // optional (tools/trace_flow.py): per-strip timestamps, else null

@@ -181,7 +181,8 @@ def test_slab_edges_are_system_scope():
     slab_kernels = {"sw_flow3rs_kernel", "sw_flow3ras_kernel", "sw_flow3r3s_kernel", "sw_flow3ra3s_kernel"}
     other_kernels = {"sw_flow3_kernel", "sw_flow3a_kernel", "sw_flow3p_kernel", "sw_flow3r_kernel",
                      "sw_flow3ra_kernel", "sw_flow3r3_kernel", "sw_flow3ra3_kernel", "sw_flow3r45_kernel",
-                     "sw_flow3r3p_kernel", "sw_flow3ra3p_kernel", "sw_flow3h_kernel", "sw_flow3ah_kernel"}
+                     "sw_flow3r3p_kernel", "sw_flow3ra3p_kernel", "sw_flow3h_kernel", "sw_flow3ah_kernel",
+                     "sw_flow3r3h_kernel", "sw_flow3ra3h_kernel"}
     found = {}
     for name, body in funcs.items():
         m = re.search(r"\d(sw_flow3[a-z0-9]*_kernel)", name)

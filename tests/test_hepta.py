@@ -8,8 +8,9 @@ alphabet.
 Covered: alphabets of 1..7 values (0x00 and 0xFF among them), the linear-gap (two columns per
 lane) and affine (one column) staged kernels at C = 32 with half-chunk links and at C = 16,
 ragged strips, the host entry points and the device entry point (the alphabet kernel's byte
-set); fallbacks to the byte path: eight values, option hep = 0, rows too long for LDS, the
-pool loops; a C2-size ACGTN pair against the byte path."""
+set); the three-column ring kernels (rows too long for LDS, or option ring = 1) over rows translated
+to selectors; fallbacks to the byte path: eight values, option hep = 0, the pool loops; C2- and
+C5-size ACGTN pairs against the byte path."""
 import numpy as np
 import pytest
 
@@ -42,7 +43,7 @@ def _related(rng, alpha, n, m, p=0.15):
 @pytest.fixture(autouse=True)
 def _defaults(engine):
     yield
-    for k, v in (("hep", 1), ("C", 0), ("W", 0), ("f3hl", 1), ("f3pool", 0), ("mode", -1)):
+    for k, v in (("hep", 1), ("C", 0), ("W", 0), ("f3hl", 1), ("f3pool", 0), ("mode", -1), ("ring", -1)):
         engine.set_option(k, v)
 
 
@@ -131,3 +132,39 @@ def test_hepta_c2_size_acgtn(engine):
     ref = engine.SmithWatermanScoreCUDA(a, b)
     assert engine.last_stats()["dna"] == 0
     assert got == ref
+
+
+@pytest.mark.parametrize("prm_t", [(1, -1, 1, 1), (2, -3, 5, 2)])
+def test_hepta_ring_mode(engine, oracle_mod, prm_t):
+    """Ring mode (option ring = 1 on pairs the oracle scores in seconds): the three-column ring
+    kernels over seven-letter rows translated to selectors (sw_flow3r3h / ra3h_kernel), ragged
+    shapes, equal to the oracle."""
+    rng = np.random.default_rng(17 + prm_t[0])
+    op = oracle_mod.Params(*prm_t)
+    engine.set_option("ring", 1)
+    try:
+        for k, (n, m) in enumerate([(5000, 3000), (12000, 9000), (800, 20000)]):
+            alpha = (ALPHABETS["acgtn"], ALPHABETS["seven"], ALPHABETS["rna"])[k]
+            a, b = _related(rng, alpha, n, m, 0.1) if k != 1 else (_rand(rng, alpha, n), _rand(rng, alpha, m))
+            got, st = _score(engine, a, b, engine.Params(*prm_t))
+            assert st["dna"] == 2 and st["variant"] & 4 and st["variant"] & 8192, st   # ring, three columns
+            assert got == oracle_mod.score_linear(a, b, op), (prm_t, n, m)
+    finally:
+        engine.set_option("ring", -1)
+
+
+def test_hepta_c5_size_acgtn(engine):
+    """N = 2^20 with 1 % N (C5's shape, ring mode by size): the seven-letter ring kernel equals the
+    byte path (hep = 0)."""
+    rng = np.random.default_rng(1 << 20)
+    a, b = engine.gen_pair(1 << 20, 1 << 20)
+    a, b = a.copy(), b.copy()
+    a[rng.random(1 << 20) < 0.01] = ord("N")
+    b[rng.random(1 << 20) < 0.01] = ord("N")
+    got = engine.SmithWatermanScoreCUDA(a, b)
+    st = engine.last_stats()
+    assert st["dna"] == 2 and st["variant"] & 4 and st["variant"] & HEP_BIT, st
+    engine.set_option("hep", 0)
+    ref = engine.SmithWatermanScoreCUDA(a, b)
+    assert engine.last_stats()["dna"] == 0
+    assert got == ref and got > 100000

@@ -517,7 +517,7 @@ def ring_gin_check(a, C=64, key="%[ek]"):
     a("s_cmp_lg_u64 s[50:51], 0")
 
 
-def gen_role_ring(IN, OUT_, C=64, hl=False, W=2):
+def gen_role_ring(IN, OUT_, C=64, hl=False, W=2, hep=False):
     """The ring-mode loop of one strip role at C-row chunks (64, or 32: half the hand-off
     lag).  The loop body is two chunks; the code ring is refilled 64 rows per body.
     hl (C = 64): half-chunk LDS links as in gen_role: the producer also publishes its newest
@@ -525,7 +525,10 @@ def gen_role_ring(IN, OUT_, C=64, hl=False, W=2):
     write-ahead slots 64 rows on (%[lmid] from the ring offset of chunk k0 + 64); the consumer
     starts a chunk on its first 32 rows and merges the other 32 into lanes 0..31 at mid-chunk.
     Words count rows available - 32; the back-pressure floor is k0 + 64 (the next mid-chunk's
-    write-ahead)."""
+    write-ahead).
+    hep: a pair over up to seven byte values (sw_flow3.hip HEP): the streamed rows are already
+    perm selectors (translated by the engine; 0 past the last row), so the refill writes them
+    as they are, and the perms take each column's low word %[qA] / %[qB] / %[qC]."""
     L = []
     a = L.append
     lds_in, lds_out = IN == "lds", OUT_ == "lds"
@@ -628,12 +631,15 @@ def gen_role_ring(IN, OUT_, C=64, hl=False, W=2):
         # 4. codes of 64 rows (128..191 ahead of the body's first row) into the wave's code
         # ring (slot base s53, mirror of slots [0, 64))
         if refill:
-            a("v_lshrrev_b32 v94, 1, v93")
-            a("v_lshrrev_b32 v103, 2, v93")
-            a("v_xor_b32 v94, v94, v103")
-            a("v_and_or_b32 v94, v94, 3, 4")
-            a("v_cmp_ne_u32_e64 s[56:57], 0, v93")
-            a("v_cndmask_b32_e64 v94, 0, v94, s[56:57]")
+            if hep:
+                a("v_mov_b32 v94, v93")
+            else:
+                a("v_lshrrev_b32 v94, 1, v93")
+                a("v_lshrrev_b32 v103, 2, v93")
+                a("v_xor_b32 v94, v94, v103")
+                a("v_and_or_b32 v94, v94, 3, 4")
+                a("v_cmp_ne_u32_e64 s[56:57], 0, v93")
+                a("v_cndmask_b32_e64 v94, 0, v94, s[56:57]")
             a("v_add_u32 v95, s53, %[cwr]")
             a("ds_write_b8 v95, v94")
             a("s_cmp_eq_u32 s53, 0")
@@ -703,10 +709,11 @@ def gen_role_ring(IN, OUT_, C=64, hl=False, W=2):
                     a(f"L_midr{p}_%=:")
                     a(f"s_waitcnt lgkmcnt({2 if lds_out else 0})")
                     a("v_cndmask_b32_e64 v40, v102, v40, %[lhi]")
-            a(f"v_perm_b32 v48, %[pA], %[k80], v{cur + u}")
-            a(f"v_perm_b32 v49, %[pB], %[k80], v{cur + u}")
+            qa, qb, qc = ("%[qA]", "%[qB]", "%[qC]") if hep else ("%[k80]",) * 3
+            a(f"v_perm_b32 v48, %[pA], {qa}, v{cur + u}")
+            a(f"v_perm_b32 v49, %[pB], {qb}, v{cur + u}")
             if W >= 3:
-                a(f"v_perm_b32 v112, %[pC], %[k80], v{cur + u}")
+                a(f"v_perm_b32 v112, %[pC], {qc}, v{cur + u}")
             if W >= 4:
                 a(f"v_perm_b32 v116, %[pD], %[k80], v{cur + u}")
             if W == 5:
@@ -896,20 +903,28 @@ def emit_ring3():
     # ALN = 1 (the column-slab kernel, one wave per SIMD): every 8-B instruction on an 8-B boundary,
     # padding with s_nop (slab 0 of 8: 32.5 -> 29.5 ms); ALN = 0 (C5, 4 waves per SIMD): as generated
     # (aligned there: 154.3 -> 161.1 ms with nops, 163.0 with VOP3 re-encodings)
+    # HEP (aln 2 below): the ring roles of a pair over up to seven byte values (sw_flow3r3h_kernel)
     combos = [(i, o, 0) for i in ROLES_IN_RING for o in ROLES_OUT] + \
-        [(i, o, 1) for i in ROLES_IN_RING for o in ROLES_OUT] + [(i, o, 1) for i, o in ROLES_SLAB]
+        [(i, o, 1) for i in ROLES_IN_RING for o in ROLES_OUT] + [(i, o, 1) for i, o in ROLES_SLAB] + \
+        [(i, o, 2) for i in ROLES_IN_RING for o in ROLES_OUT]
     for IN, OUT_, aln in combos:
-        body = gen_role_ring(IN, OUT_, 64, False, 3)
-        if aln:
+        hep = aln == 2
+        body = gen_role_ring(IN, OUT_, 64, False, 3, hep)
+        if aln == 1:
             body = align8(body, nops=True, promote=False)
-        out.append("template <> __device__ __forceinline__ F3Res f3r3_loop<F3_%s, F3_%s, %d>(const F3RLoop& x) {"
-                   % (IN.upper(), OUT_.upper(), aln))
+        if hep:
+            out.append("template <> __device__ __forceinline__ F3Res f3r3h_loop<F3_%s, F3_%s>(const F3RLoop& x) {"
+                       % (IN.upper(), OUT_.upper()))
+        else:
+            out.append("template <> __device__ __forceinline__ F3Res f3r3_loop<F3_%s, F3_%s, %d>(const F3RLoop& x) {"
+                       % (IN.upper(), OUT_.upper(), aln))
         out.append("    F3Res r;")
         out.append("    asm volatile(")
         for line in body:
             out.append('        "%s\\n\\t"' % line)
         out.append('        : [M] "=v"(r.M), [fail] "=s"(r.fail), [slow] "=s"(r.slow)')
-        out.append('        : [pA] "v"(x.pA), [pB] "v"(x.pB), [pC] "v"(x.pC), [ng] "v"(x.ng), [G] "s"(x.G), [k80] "s"(x.k80),')
+        out.append('        : [pA] "v"(x.pA), [pB] "v"(x.pB), [pC] "v"(x.pC), [ng] "v"(x.ng), [G] "s"(x.G), ' +
+                   ('[qA] "v"(x.qA), [qB] "v"(x.qB), [qC] "v"(x.qC),' if hep else '[k80] "s"(x.k80),'))
         out.append('          [m] "s"(x.m), [end] "s"(x.end), [dlo] "s"(x.dlo), [dhi] "s"(x.dhi), [lane] "v"(x.lane),')
         out.append('          [raw2] "v"(x.raw2), [cro] "v"(x.cro), [c0] "v"(x.c0), [cbase] "v"(x.cbase),')
         out.append('          [cwr] "v"(x.cwr), [cwm] "v"(x.cwm), [rrs] "s"(x.rrs), [rrow] "v"(x.rrow),')
@@ -1336,9 +1351,9 @@ def ring_gin_check_aff(a, key="%[ek]", key2="%[ek2]"):
     a("s_cmp_lg_u64 s[50:51], 0")
 
 
-def gen_role_ring_aff(IN, OUT_, W=2):
+def gen_role_ring_aff(IN, OUT_, W=2, hep=False):
     """gen_role_ring (C = 64, whole-chunk links) around the two-column affine step (W = 3: the
-    three-column one, step_aff3)."""
+    three-column one, step_aff3); hep as gen_role_ring."""
     C = 64
     L = []
     a = L.append
@@ -1422,12 +1437,15 @@ def gen_role_ring_aff(IN, OUT_, W=2):
             a("v_mov_b32 v40, %[ng]")
             a("v_mov_b32 v41, %[nge]")
         # codes of 64 rows (128..191 ahead of the body's first row) into the wave's code ring
-        a("v_lshrrev_b32 v102, 1, v101")
-        a("v_lshrrev_b32 v113, 2, v101")
-        a("v_xor_b32 v102, v102, v113")
-        a("v_and_or_b32 v102, v102, 3, 4")
-        a("v_cmp_ne_u32_e64 s[56:57], 0, v101")
-        a("v_cndmask_b32_e64 v102, 0, v102, s[56:57]")
+        if hep:
+            a("v_mov_b32 v102, v101")
+        else:
+            a("v_lshrrev_b32 v102, 1, v101")
+            a("v_lshrrev_b32 v113, 2, v101")
+            a("v_xor_b32 v102, v102, v113")
+            a("v_and_or_b32 v102, v102, 3, 4")
+            a("v_cmp_ne_u32_e64 s[56:57], 0, v101")
+            a("v_cndmask_b32_e64 v102, 0, v102, s[56:57]")
         a("v_add_u32 v103, s53, %[cwr]")
         a("ds_write_b8 v103, v102")
         a("s_cmp_eq_u32 s53, 0")
@@ -1471,10 +1489,11 @@ def gen_role_ring_aff(IN, OUT_, W=2):
         else:
             a(f"s_waitcnt lgkmcnt({len(lds)})")
         for u in range(C // 4):
-            a(f"v_perm_b32 v55, %[pA], %[k80], v{cur + u}")
-            a(f"v_perm_b32 v56, %[pB], %[k80], v{cur + u}")
+            qa, qb, qc = ("%[qA]", "%[qB]", "%[qC]") if hep else ("%[k80]",) * 3
+            a(f"v_perm_b32 v55, %[pA], {qa}, v{cur + u}")
+            a(f"v_perm_b32 v56, %[pB], {qb}, v{cur + u}")
             if W == 3:
-                a(f"v_perm_b32 v124, %[pC], %[k80], v{cur + u}")
+                a(f"v_perm_b32 v124, %[pC], {qc}, v{cur + u}")
             for b in range(4):
                 (step_aff3 if W == 3 else step_aff2)(a, b, b % 2 == 0)
             if gout and u == 7:
@@ -1578,16 +1597,22 @@ def emit_ring_aff():
            "// Operands: see F3RALoop in sw_flow3.hip; fixed registers: tools/gen_flow3.py (gen_role_ring_aff).",
            "#pragma once", ""]
     ring_roles = [(i, o) for i in ROLES_IN_RING for o in ROLES_OUT]
+    # aln 2: the W3 ring roles of a pair over up to seven byte values (f3ra3h_loop, sw_flow3ra3h_kernel)
     combos = [(i, o, 2, 0) for i, o in ring_roles + list(ROLES_SLAB)] + \
-        [(i, o, 3, 0) for i, o in ring_roles] + [(i, o, 3, 1) for i, o in ring_roles + list(ROLES_SLAB)]
+        [(i, o, 3, 0) for i, o in ring_roles] + [(i, o, 3, 1) for i, o in ring_roles + list(ROLES_SLAB)] + \
+        [(i, o, 3, 2) for i, o in ring_roles]
     for IN, OUT_, W, aln in combos:
-        body = gen_role_ring_aff(IN, OUT_, W)
+        hep = aln == 2
+        body = gen_role_ring_aff(IN, OUT_, W, hep)
         if W == 2 and RING_ALIGN:
             body = align8(body, nops=RING_NOPS)
-        if aln:
+        if aln == 1:
             body = align8(body, nops=True, promote=False)
         if W == 2:
             out.append("template <> __device__ __forceinline__ F3Res f3ra_loop<F3_%s, F3_%s>(const F3RALoop& x) {"
+                       % (IN.upper(), OUT_.upper()))
+        elif hep:
+            out.append("template <> __device__ __forceinline__ F3Res f3ra3h_loop<F3_%s, F3_%s>(const F3RALoop& x) {"
                        % (IN.upper(), OUT_.upper()))
         else:
             out.append("template <> __device__ __forceinline__ F3Res f3ra3_loop<F3_%s, F3_%s, %d>(const F3RALoop& x) {"
@@ -1599,7 +1624,8 @@ def emit_ring_aff():
         out.append('        : [M] "=v"(r.M), [fail] "=s"(r.fail), [slow] "=s"(r.slow)')
         out.append('        : [pA] "v"(x.pA), [pB] "v"(x.pB), [ng] "v"(x.ng), [nge] "v"(x.nge), [GI] "s"(x.GI),' if W == 2 else
                    '        : [pA] "v"(x.pA), [pB] "v"(x.pB), [pC] "v"(x.pC), [ng] "v"(x.ng), [nge] "v"(x.nge), [GI] "s"(x.GI),')
-        out.append('          [GE] "s"(x.GE), [k80] "s"(x.k80), [m] "s"(x.m), [end] "s"(x.end), [dlo] "s"(x.dlo),')
+        out.append('          [GE] "s"(x.GE), ' + ('[qA] "v"(x.qA), [qB] "v"(x.qB), [qC] "v"(x.qC),' if hep else '[k80] "s"(x.k80),') +
+                   ' [m] "s"(x.m), [end] "s"(x.end), [dlo] "s"(x.dlo),')
         out.append('          [dhi] "s"(x.dhi), [lane] "v"(x.lane), [raw2] "v"(x.raw2), [cro] "v"(x.cro), [c0] "v"(x.c0),')
         out.append('          [cbase] "v"(x.cbase), [cwr] "v"(x.cwr), [cwm] "v"(x.cwm), [rrs] "s"(x.rrs), [rrow] "v"(x.rrow),')
         out.append('          [lin] "v"(x.lin), [lout] "v"(x.lout), [pin] "v"(x.pin), [pout] "v"(x.pout),')
