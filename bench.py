@@ -285,7 +285,8 @@ def kernel_label(st):
                 ("s" if v & 2048 else "") + "_kernel"
             if v & 65536:   # a pair over up to seven byte values (sw_flow3h / sw_flow3ah_kernel)
                 name += ", seven-letter alphabet"
-                fn = "sw_flow3ah_kernel" if aff3 else "sw_flow3h_kernel"
+                fn = ("sw_flow3r%s3h_kernel" % ("a" if aff3 else "")) if ring else \
+                    "sw_flow3ah_kernel" if aff3 else "sw_flow3h_kernel"
             if v & 2048:
                 name += ", column slab (peer edges)"
         else:
@@ -382,6 +383,57 @@ def batch_affine_runs(sw, torch, gold, steps, params, cells):
     return out
 
 
+def alphabet_runs(sw, torch, gold, steps):
+    """N = 1 extras: the config pairs with their bases relabeled to lower case (a, c, g, t: bytes
+    outside {A,C,G,T}, a bijection, so the reference scores and the goldens are unchanged; main.cpp
+    scores by byte equality).  C2 and C5 then take the seven-letter kernels (one pair, the alphabet
+    scanned on the device each call: sw_flow3h_kernel / sw_flow3r3h_kernel), C3 the duo kernel with
+    the penalty from the raw bytes (SW_FLAG_BYTES, no scan); each against its golden."""
+    lower = np.arange(256, dtype=np.uint8)
+    for ch in b"ACGT":
+        lower[ch] = ch + 32
+    out = {"relabel": "A,C,G,T -> a,c,g,t (bytes outside {A,C,G,T}; goldens unchanged)"}
+    stream = torch.cuda.current_stream()
+    for key, N, seed, gk, nsteps in (("c2_lower", 65536, 65536, "C2", steps), ("c5_lower", 1 << 20, 1 << 20, "C5", 2)):
+        a, b = sw.gen_pair(seed, N)
+        arena = torch.from_numpy(np.concatenate([lower[a], lower[b]])).cuda()
+        scores = torch.zeros(1, dtype=torch.int32, device="cuda")
+
+        def launch():
+            sw.score_batch_device(arena.data_ptr(), [0], [N], [N], [N], scores.data_ptr(), flags=0,
+                                  stream=stream.cuda_stream)
+        t, k = time_launches(torch, launch, lambda: None, nsteps, 1, stream, None)
+        sw.stream_status(stream.cuda_stream)
+        st = sw.last_stats()
+        g = gold.get(gk, {})
+        out[key] = {"N": N, "ms_per_step": round(t / nsteps * 1e3, 4), "value": round(N * N * nsteps / t / 1e9, 3),
+                    "unit": "GCUPS", "kernel_ms_per_launch": round(k, 4), "steps": nsteps,
+                    "parity": ("ok" if scores[0].item() == g["score"] else "MISMATCH") if g else "unchecked",
+                    "golden": gk, "alphabet": "seven-letter path" if st["dna"] == 2 else "dna %d" % st["dna"],
+                    "timed": "device entry incl. the alphabet scan and its host sync per call", **kernel_label(st)}
+    host = lower[sw.gen_batch(8192, 1024, 8192)]
+    arena = torch.from_numpy(host).cuda()
+    scores = torch.zeros(1024, dtype=torch.int32, device="cuda")
+    offs_a = [2 * 8192 * k for k in range(1024)]
+    offs_b = [2 * 8192 * k + 8192 for k in range(1024)]
+
+    def launch_b():
+        sw.score_batch_device(arena.data_ptr(), offs_a, [8192] * 1024, offs_b, [8192] * 1024, scores.data_ptr(),
+                              flags=sw.SW_FLAG_BYTES, stream=stream.cuda_stream)
+    bsteps = max(3, steps // 2)
+    t, k = time_launches(torch, launch_b, lambda: None, bsteps, 1, stream, None)
+    sw.stream_status(stream.cuda_stream)
+    st = sw.last_stats()
+    ref = gold.get("C3", {}).get("scores", [])
+    cells = 1024 * 8192 * 8192
+    out["c3_lower"] = {"ms_per_step": round(t / bsteps * 1e3, 4), "value": round(cells * bsteps / t / 1e9, 3),
+                       "unit": "GCUPS", "kernel_ms_per_launch": round(k, 4), "steps": bsteps,
+                       "parity": ("ok" if scores.cpu().tolist() == ref else "MISMATCH") if len(ref) == 1024 else "unchecked",
+                       "golden": "C3 (all 1024 pairs)", "alphabet": "raw bytes" if st["dna"] == 0 else "dna %d" % st["dna"],
+                       **kernel_label(st)}
+    return out
+
+
 def c5_runs(sw, torch, gold, steps):
     """N = 1 extras: config C5 (one pair N = 2^20, seed 1048576, O(N) device state) with the
     reference's constants and with AFFINE_PARAMS, each against its golden."""
@@ -438,6 +490,9 @@ def headline_summary(out):
         c = (out.get("c5") or {}).get(k)
         if isinstance(c, dict):
             res["c5" if k == "linear" else "c5_affine"] = row(c)
+    for k, c in (out.get("byte_alphabets") or {}).items():
+        if isinstance(c, dict):
+            res[k] = row(c)
     res["units"] = "[ms_per_step, GCUPS, parity]"
     return res
 
@@ -724,6 +779,7 @@ def main():
 
     extra = None
     c5 = None
+    alpha = None
     affine = None
     step_ns = None
     host_api = None
@@ -853,6 +909,10 @@ def main():
         if workload == "pair" and world == 1 and args.workload == "auto" and not args.no_extra and \
                 not args.no_c5 and defaults and N == 65536:
             c5 = c5_runs(sw, torch, gold, 2)
+        alpha = None
+        if workload == "pair" and world == 1 and args.workload == "auto" and not args.no_extra and \
+                not args.no_c5 and defaults and N == 65536:
+            alpha = alphabet_runs(sw, torch, gold, args.steps)
         # the batched config measured right after on the same ranks, as an extra key:
         # C3 at N=1, 1024 pairs per GPU sharded + RCCL-gathered at N>1 (C4 at N=8)
         if workload == "pair" and args.workload == "auto" and not args.no_extra:
@@ -938,6 +998,8 @@ def main():
             out["affine_step"] = affine
         if workload != "batch" and c5 is not None:
             out["c5"] = c5
+        if workload != "batch" and alpha is not None:
+            out["byte_alphabets"] = alpha
         if world == 1 and not args.no_cpu_baseline:
             try:
                 out["cpu_baseline"] = cpu_baseline(workload, cfg["N"], args.cpu_seconds, params)

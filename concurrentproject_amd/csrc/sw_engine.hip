@@ -1336,16 +1336,18 @@ int score_one(const unsigned char* s1, const unsigned char* s2, int n, int m, co
     return sc;
 }
 
-// flag[0] |= 1 when a byte outside {A,C,G,T} occurs; with set (one pair): flag[1..8] |= the byte set
-__global__ void alphabet_kernel(const unsigned char* arena, const PairDesc* pairs, int npairs, unsigned* flag, int set) {
+// flag[0] |= 1 when a byte outside {A,C,G,T} occurs; with set (one pair): flag[1..8] |= the byte set.
+// Pair blockIdx.x / per, its n + m bytes split over `per` blocks.
+__global__ void alphabet_kernel(const unsigned char* arena, const PairDesc* pairs, int npairs, unsigned* flag, int set,
+                                int per) {
     __shared__ unsigned bits[8];
-    const int k = blockIdx.x;
+    const int k = (int)blockIdx.x / per, slice = (int)blockIdx.x % per;
     if (k >= npairs) return;
     if (threadIdx.x < 8) bits[threadIdx.x] = 0u;
     __syncthreads();
     const PairDesc d = pairs[k];
     unsigned bad = 0;
-    for (int i = threadIdx.x; i < d.n + d.m; i += blockDim.x) {
+    for (int i = slice * blockDim.x + threadIdx.x; i < d.n + d.m; i += per * blockDim.x) {
         const unsigned char ch = i < d.n ? arena[d.col_off + i] : arena[d.row_off + (i - d.n)];
         const bool b = !(ch == 'A' || ch == 'C' || ch == 'G' || ch == 'T');
         bad |= b;
@@ -1785,7 +1787,12 @@ int sw_score_batch_device(const unsigned char* d_arena, const int64_t* a_off, co
         std::memcpy(c->hdesc.p, job.pairs.data(), np * sizeof(PairDesc));
         HIPCHK(hipMemcpyAsync(c->desc.p, c->hdesc.p, np * sizeof(PairDesc), hipMemcpyHostToDevice, s));
         HIPCHK(hipMemsetAsync(c->flag.p, 0, 9 * sizeof(unsigned), s));
-        hipLaunchKernelGGL(alphabet_kernel, dim3((unsigned)np), dim3(256), 0, s, d_arena, c->desc.p, (int)np, c->flag.p, set);
+        // one pair: its bytes over up to 128 blocks (a C5 pair is 2 MB); a batch: one block per pair
+        long long longest = 0;
+        for (const PairDesc& d : job.pairs) longest = std::max(longest, (long long)d.n + d.m);
+        const int per = np == 1 ? (int)std::max(1LL, std::min(128LL, longest / 8192)) : 1;
+        hipLaunchKernelGGL(alphabet_kernel, dim3((unsigned)(np * per)), dim3(256), 0, s, d_arena, c->desc.p, (int)np,
+                           c->flag.p, set, per);
         HIPCHK(hipGetLastError());
         unsigned* hflag = reinterpret_cast<unsigned*>(c->hctrl.p);
         HIPCHK(hipMemcpyAsync(hflag, c->flag.p, 9 * sizeof(unsigned), hipMemcpyDeviceToHost, s));
