@@ -545,8 +545,12 @@ int finalize_alphabet(Job& job, const Params& prm, int cus, bool single) {
     if (job.hep) job.dna = true;
     if (finalize_mode(job, prm, cus)) return -1;
     if (!job.hep || hep_launchable(job, prm)) return 0;
-    job.hep = 0;
-    job.dna = false;
+    // a fresh job (the DNA attempt left its ring / column / stream flags behind) on the byte path
+    Job bytes;
+    bytes.pairs = job.pairs;
+    bytes.slab = job.slab;
+    bytes.dna = false;
+    job = std::move(bytes);
     const int W = pick_W(job.pairs, single);
     plan(job, W, pick_C(W), single);
     return finalize_mode(job, prm, cus);

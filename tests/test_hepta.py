@@ -43,7 +43,7 @@ def _related(rng, alpha, n, m, p=0.15):
 @pytest.fixture(autouse=True)
 def _defaults(engine):
     yield
-    for k, v in (("hep", 1), ("C", 0), ("W", 0), ("f3hl", 1), ("f3pool", 0), ("mode", -1), ("ring", -1)):
+    for k, v in (("hep", 1), ("C", 0), ("W", 0), ("f3hl", 1), ("f3pool", 0), ("mode", -1), ("ring", -1), ("f3rhl", 0)):
         engine.set_option(k, v)
 
 
@@ -84,7 +84,8 @@ def test_hepta_chunk_forms(engine, oracle_mod, C, hl):
 
 
 def test_hepta_fallbacks(engine, oracle_mod):
-    """Eight byte values, option hep = 0 and the pool loops keep the byte path; all equal."""
+    """Eight byte values, option hep = 0, the pool loops and a ring plan without a seven-letter form keep the
+    byte path; all equal."""
     rng = np.random.default_rng(3)
     a, b = _related(rng, b"ACGTacgt", 3000, 2500)
     got, st = _score(engine, a, b, engine.Params())
@@ -99,6 +100,13 @@ def test_hepta_fallbacks(engine, oracle_mod):
     engine.set_option("f3pool", 1)
     got, st = _score(engine, a, b, engine.Params())
     assert st["dna"] == 0 and got == exp, st
+    # a ring plan without the seven-letter form (half-chunk ring links: two columns per lane) re-plans
+    # from scratch on the byte path
+    engine.set_option("f3pool", 0)
+    engine.set_option("ring", 1)
+    engine.set_option("f3rhl", 1)
+    got, st = _score(engine, a, b, engine.Params())
+    assert st["dna"] == 0 and not st["variant"] & 4 and got == exp, st
 
 
 def test_hepta_device_entry(engine, oracle_mod):
