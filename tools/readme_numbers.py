@@ -13,7 +13,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 BEGIN, END = "<!-- NUMBERS BEGIN (tools/readme_numbers.py) -->", "<!-- NUMBERS END -->"
 LABEL = {"c2": "C2, one pair N = 65536 (the headline `value`)", "c2_affine": "C2 with G_INIT != G_EXT (2, -3, 5, 2)",
          "c3": "C3, 1024 pairs N = 8192", "c3_affine": "C3 with (2, -3, 5, 2)", "c5": "C5, one pair N = 2^20",
-         "c5_affine": "C5 with (2, -3, 5, 2)"}
+         "c5_affine": "C5 with (2, -3, 5, 2)", "c2_lower": "C2 relabeled a, c, g, t (seven-letter kernels)",
+         "c5_lower": "C5 relabeled a, c, g, t (seven-letter ring kernel)",
+         "c3_lower": "C3 relabeled a, c, g, t (duo on raw bytes)"}
 
 
 def fmt_ms(x):
