@@ -18,9 +18,12 @@ struct sw_db {
     std::vector<int> order;             // record indices, longest first
     int dna = -1;                       // every residue in {A,C,G,T}: 1 / 0, -1 not scanned yet (sw_db.hip)
     struct Dev {
-        unsigned char* arena = nullptr; // residues, then qcap bytes of query slot
+        unsigned char* arena = nullptr; // residues, then two query slots of qcap bytes
         size_t qcap = 0;
-        int* scores = nullptr;
+        int* scores = nullptr;          // two score buffers of the record count (sw_db_search_db alternates)
+        int* hscores = nullptr;         // pinned host copies of both
+        void* stream = nullptr;         // sw_db_search_db's hipStream_t (queries pipelined on it; sw_db.hip)
+        void* done[2] = {nullptr, nullptr};   // its hipEvent_t per score buffer
     };
     std::map<int, Dev> dev;             // per device ordinal (sw_db.hip)
     std::mutex mu;                      // one search at a time per database

@@ -220,3 +220,29 @@ def test_search_dna_duo_path(engine, oracle_mod):
     db = engine.Database.from_records(recs)
     q = ACGT[rng.integers(0, 4, 2048)].tobytes()
     assert db.search(q).tolist() == _expect(oracle_mod, q, recs)
+
+
+@pytest.mark.gpu
+def test_search_db_pipelined(engine, oracle_mod):
+    """sw_db_search_db runs its queries pipelined on the database's stream (two query slots and score
+    buffers, the next query planned while one runs): 9 queries of ragged lengths, one empty, DNA and
+    non-DNA ones alternating the alphabet path, against one search per query and the oracle."""
+    rng = np.random.default_rng(12)
+    acgt = np.frombuffer(b"ACGT", np.uint8)
+    recs = [("r%d" % i, acgt[rng.integers(0, 4, int(rng.integers(50, 900)))].tobytes()) for i in range(300)]
+    queries = []
+    for k in range(9):
+        n = 0 if k == 4 else int(rng.integers(30, 700))
+        q = acgt[rng.integers(0, 4, n)]
+        if k % 3 == 1 and n:
+            q = q.copy()
+            q[::7] = ord("N")
+        queries.append(("q%d" % k, q.tobytes()))
+    db = engine.Database.from_records(recs)
+    qs = engine.Database.from_records(queries)
+    got = db.search_db(qs)
+    assert got.shape == (9, 300)
+    for k, (_, q) in enumerate(queries):
+        assert got[k].tolist() == db.search(q).tolist(), k
+    for k in (0, 1, 4, 8):
+        assert got[k].tolist() == _expect(oracle_mod, queries[k][1], recs), k

@@ -28,6 +28,8 @@ def main():
     ap.add_argument("--hi", type=int, default=4096)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--alphabet", default="dna", choices=("dna", "protein"))
+    ap.add_argument("--queries", type=int, default=0,
+                    help="also time search_db over this many queries of qlen (pipelined on the database's stream)")
     ap.add_argument("--opt", action="append", default=[], help="engine option k=v (sw_set_option), repeatable")
     a = ap.parse_args()
     import concurrentproject_amd as sw
@@ -54,6 +56,23 @@ def main():
                       "unit": "GCUPS", "ms_per_search": round(dt * 1e3, 3), "records": a.records,
                       "residues": int(lens.sum()), "qlen": a.qlen, "len_range": [a.lo, a.hi],
                       "max_score": int(sc.max())}))
+    if a.queries:
+        from concurrentproject_amd.db import Database as D
+        qrecs = [("q%d" % k, acgt[rng.integers(0, len(acgt), size=a.qlen)].tobytes()) for k in range(a.queries)]
+        qdb = D.from_records(qrecs)
+        db.search_db(qdb)   # warm
+        t0 = time.perf_counter()
+        many = db.search_db(qdb)
+        dm = (time.perf_counter() - t0) / a.queries
+        t0 = time.perf_counter()
+        one = [db.search(q) for _, q in qrecs]
+        ds = (time.perf_counter() - t0) / a.queries
+        print(json.dumps({"metric": "db search_db GCUPS (host API, pipelined queries)", "alphabet": a.alphabet,
+                          "queries": a.queries, "ms_per_query": round(dm * 1e3, 3),
+                          "value": round(cells / dm / 1e9, 2), "unit": "GCUPS",
+                          "ms_per_query_one_by_one": round(ds * 1e3, 3),
+                          "equal": all(many[k].tolist() == one[k].tolist() for k in range(a.queries))}))
+        qdb.close()
     db.close()
 
 
